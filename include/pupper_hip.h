@@ -1,0 +1,344 @@
+/*
+ * pupper_hip.h -- C-ABI of the MI355X-native Pupper-v3 environment.
+ *
+ * This is the drop-in boundary for the hot path named by BASELINE.json
+ * `north_star`: the batched replacement for
+ *
+ *   pupperv3_mjx.environment.PupperV3Env.reset(rng)  (environment.py:314-346)
+ *   pupperv3_mjx.environment.PupperV3Env.step(state, action)  (environment.py:348-483)
+ *
+ * including the MJX physics they call (`pipeline_init` environment.py:319,
+ * `pipeline_step` environment.py:366 -> 5 x mjx.step), the reward stack
+ * (rewards.py:9-138), the observation pipeline (environment.py:485-543) and the
+ * per-env domain randomisation (domain_randomization.py:8-112).
+ *
+ * Plain C types only: pointers + sizes, int status codes, no exceptions and no
+ * torch types across the boundary.  All `*_dev` arguments are device pointers
+ * on the handle's device; `stream` is a hipStream_t passed as void* (NULL =
+ * the handle's own stream).
+ *
+ * The reference's FFI for this path is Python (Brax `Env.reset/step`,
+ * [ext] brax 0.12.1 brax/envs/base.py); the ctypes binding a maintainer adds is
+ * shown in INTEGRATION.md and implemented in pupperv3-mjx_amd/pupperv3_mjx/_lib.py.
+ */
+#ifndef PUPPER_HIP_H_
+#define PUPPER_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PP3_ABI_VERSION 1
+
+/* ---- fixed topology of test_pupper_model.xml (checked at pp3_create) ---- */
+#define PP3_NBODY 14      /* world + base_link + 4 legs x 3 links          */
+#define PP3_NJNT 13       /* 1 free joint + 12 hinges                      */
+#define PP3_NQ 19
+#define PP3_NV 18
+#define PP3_NU 12
+#define PP3_NLEG 4
+#define PP3_NFOOT 4
+#define PP3_MAX_CGEOM 96  /* collidable geoms (8 spheres + floor + boxes)  */
+#define PP3_MAX_PAIR 640  /* candidate collision pairs after filtering     */
+#define PP3_MAX_SITE 8
+#define PP3_MAX_LAG 8     /* latency-buffer length limit                   */
+#define PP3_NREWARD 18    /* reward terms, order = PP3_REWARD_* below      */
+#define PP3_NMETRIC 19    /* total_dist + 18 scaled reward terms           */
+#define PP3_NDR 62        /* per-env domain-randomisation scalars          */
+#define PP3_OBS_DIM 36    /* environment.py:226                            */
+
+/* MuJoCo enums restated (mjtGeom / mjtJoint / mjtCone / mjtBias) */
+enum { PP3_GEOM_PLANE = 0, PP3_GEOM_SPHERE = 2, PP3_GEOM_BOX = 6 };
+enum { PP3_JNT_FREE = 0, PP3_JNT_HINGE = 3 };
+enum { PP3_CONE_PYRAMIDAL = 0 };
+enum { PP3_BIAS_NONE = 0, PP3_BIAS_AFFINE = 1 };
+
+/* Reward-term order = the rewards_dict literal in environment.py:391-444
+ * (this order is also the fp32 summation order of environment.py:446). */
+enum {
+  PP3_REWARD_TRACKING_LIN_VEL = 0,
+  PP3_REWARD_TRACKING_ANG_VEL,
+  PP3_REWARD_TRACKING_ORIENTATION,
+  PP3_REWARD_LIN_VEL_Z,
+  PP3_REWARD_ANG_VEL_XY,
+  PP3_REWARD_ORIENTATION,
+  PP3_REWARD_TORQUES,
+  PP3_REWARD_JOINT_ACCELERATION,
+  PP3_REWARD_MECHANICAL_WORK,
+  PP3_REWARD_ACTION_RATE,
+  PP3_REWARD_STAND_STILL,
+  PP3_REWARD_STAND_STILL_JOINT_VELOCITY,
+  PP3_REWARD_ABDUCTION_ANGLE,
+  PP3_REWARD_FEET_AIR_TIME,
+  PP3_REWARD_FOOT_SLIP,
+  PP3_REWARD_TERMINATION,
+  PP3_REWARD_KNEE_COLLISION,
+  PP3_REWARD_BODY_COLLISION
+};
+
+/* Compiled model (host, fp64).  Produced by the MJCF-subset compiler
+ * pupperv3_mjx/mjcf.py from test_pupper_model.xml (+ obstacles.py boxes).
+ * Field names follow mjModel. */
+typedef struct pp3_model_t {
+  /* <option> */
+  double timestep;
+  double gravity[3];
+  double impratio;
+  double tolerance;
+  double ls_tolerance;
+  int32_t iterations;
+  int32_t ls_iterations;
+  int32_t cone;
+  int32_t eulerdamp;   /* 1 = enabled; the model disables it (xml:58) */
+  double meaninertia;  /* mjStatistic.meaninertia: mean diag(M) at qpos0 */
+  /* bodies (0 = world) */
+  int32_t body_parentid[PP3_NBODY];
+  int32_t body_jntadr[PP3_NBODY];
+  int32_t body_dofadr[PP3_NBODY];
+  int32_t body_dofnum[PP3_NBODY];
+  double body_pos[PP3_NBODY][3];
+  double body_quat[PP3_NBODY][4];
+  double body_ipos[PP3_NBODY][3];
+  double body_iquat[PP3_NBODY][4];
+  double body_mass[PP3_NBODY];
+  double body_inertia[PP3_NBODY][3];
+  double body_invweight0[PP3_NBODY][2];
+  /* joints */
+  int32_t jnt_type[PP3_NJNT];
+  int32_t jnt_bodyid[PP3_NJNT];
+  int32_t jnt_qposadr[PP3_NJNT];
+  int32_t jnt_dofadr[PP3_NJNT];
+  int32_t jnt_limited[PP3_NJNT];
+  double jnt_pos[PP3_NJNT][3];
+  double jnt_axis[PP3_NJNT][3];
+  double jnt_range[PP3_NJNT][2];
+  double jnt_margin[PP3_NJNT];
+  double jnt_solref[PP3_NJNT][2];
+  double jnt_solimp[PP3_NJNT][5];
+  /* dofs */
+  int32_t dof_bodyid[PP3_NV];
+  int32_t dof_jntid[PP3_NV];
+  int32_t dof_parentid[PP3_NV];
+  double dof_armature[PP3_NV];
+  double dof_damping[PP3_NV];
+  double dof_frictionloss[PP3_NV];
+  double dof_invweight0[PP3_NV];
+  double dof_solref[PP3_NV][2];
+  double dof_solimp[PP3_NV][5];
+  double qpos0[PP3_NQ];
+  double key_qpos[PP3_NQ]; /* keyframe "home" */
+  /* collidable geoms (contype|conaffinity != 0); cgeom_id = MuJoCo geom id */
+  int32_t ngeom;  /* total MuJoCo geoms (ids) */
+  int32_t ncgeom;
+  int32_t cgeom_id[PP3_MAX_CGEOM];
+  int32_t cgeom_type[PP3_MAX_CGEOM];
+  int32_t cgeom_bodyid[PP3_MAX_CGEOM];
+  int32_t cgeom_condim[PP3_MAX_CGEOM];
+  int32_t cgeom_priority[PP3_MAX_CGEOM];
+  double cgeom_size[PP3_MAX_CGEOM][3];
+  double cgeom_pos[PP3_MAX_CGEOM][3];   /* in body frame */
+  double cgeom_quat[PP3_MAX_CGEOM][4];  /* in body frame */
+  double cgeom_friction[PP3_MAX_CGEOM][3];
+  double cgeom_solref[PP3_MAX_CGEOM][2];
+  double cgeom_solimp[PP3_MAX_CGEOM][5];
+  double cgeom_solmix[PP3_MAX_CGEOM];
+  double cgeom_margin[PP3_MAX_CGEOM];
+  double cgeom_gap[PP3_MAX_CGEOM];
+  /* candidate pairs (indices into cgeom_*), type(g1) <= type(g2) */
+  int32_t npair;
+  int32_t pair_g1[PP3_MAX_PAIR];
+  int32_t pair_g2[PP3_MAX_PAIR];
+  /* sites */
+  int32_t nsite;
+  int32_t site_bodyid[PP3_MAX_SITE];
+  double site_pos[PP3_MAX_SITE][3];
+  /* actuators (general, joint transmission) */
+  int32_t actuator_trnid[PP3_NU];  /* joint id */
+  int32_t actuator_biastype[PP3_NU];
+  int32_t actuator_forcelimited[PP3_NU];
+  int32_t actuator_ctrllimited[PP3_NU];
+  double actuator_gear[PP3_NU];
+  double actuator_gainprm[PP3_NU][3];
+  double actuator_biasprm[PP3_NU][3];
+  double actuator_forcerange[PP3_NU][2];
+  double actuator_ctrlrange[PP3_NU][2];
+  /* <custom> numerics (MJX collision caps; -1 = absent) */
+  int32_t max_contact_points;
+  int32_t max_geom_pairs;
+} pp3_model_t;
+
+/* Environment configuration: PupperV3Env.__init__ kwargs
+ * (environment.py:35-121) + config.py reward scales. */
+typedef struct pp3_env_config_t {
+  int32_t n_frames;            /* physics substeps per env step (5)        */
+  int32_t obs_history;         /* H                                         */
+  int32_t use_imu;
+  int32_t latency_len;         /* La = len(latency_distribution)           */
+  int32_t imu_latency_len;     /* Li                                        */
+  int32_t resample_velocity_step;
+  int32_t early_termination_step_threshold;
+  int32_t torso_body;
+  int32_t feet_site[PP3_NFOOT];
+  int32_t lower_leg_body[PP3_NFOOT];
+  int32_t n_upper_leg_geoms;
+  int32_t upper_leg_geoms[16];
+  int32_t n_torso_geoms;
+  int32_t torso_geoms[8];
+  int32_t rng_partitionable;   /* jax_threefry_partitionable (jax 0.5.0: 1) */
+  int32_t pad0;
+  double latency_dist[PP3_MAX_LAG];
+  double imu_latency_dist[PP3_MAX_LAG];
+  double action_scale;
+  double default_pose[PP3_NU];
+  double joint_lower[PP3_NU];
+  double joint_upper[PP3_NU];
+  double desired_abduction[4];
+  double start_pos_min[3];
+  double start_pos_max[3];
+  double lin_vel_x_range[2];
+  double lin_vel_y_range[2];
+  double ang_vel_range[2];
+  double zero_command_probability;
+  double stand_still_command_threshold;
+  double max_pitch_command;    /* degrees */
+  double max_roll_command;     /* degrees */
+  double ang_vel_noise;
+  double gravity_noise;
+  double motor_angle_noise;
+  double last_action_noise;
+  double kick_vel;
+  double kick_probability;
+  double terminal_body_z;
+  double terminal_body_angle;
+  double foot_radius;
+  double env_dt;               /* self._dt = environment_timestep          */
+  double dt;                   /* self.dt = opt.timestep * n_frames        */
+  double desired_world_z[3];
+  double reward_scales[PP3_NREWARD];
+  double tracking_sigma;
+} pp3_env_config_t;
+
+typedef struct pp3_env pp3_env_t;
+
+/* ---- per-env state record (float32 words, env-major: state[N][stride]) ---- */
+enum {
+  PP3_S_QPOS = 0,          /* 19 */
+  PP3_S_QVEL = 19,         /* 18 */
+  PP3_S_QACC_WS = 37,      /* 18  qacc_warmstart                         */
+  PP3_S_RNG = 55,          /*  2  uint32 key words, bit-cast into f32    */
+  PP3_S_LAST_ACT = 57,     /* 12 */
+  PP3_S_LAST_VEL = 69,     /* 12 */
+  PP3_S_COMMAND = 81,      /*  3 */
+  PP3_S_DESIRED_Z = 84,    /*  3 */
+  PP3_S_AIR_TIME = 87,     /*  4 */
+  PP3_S_LAST_CONTACT = 91, /*  4  0.0 / 1.0                             */
+  PP3_S_KICK = 95,         /*  2 */
+  PP3_S_STEP = 97,         /*  1  step counter (integral value as float) */
+  PP3_S_ACT_BUF = 98       /* 12*La action buffer [12][La], then 6*Li imu buffer [6][Li] */
+};
+
+/* Field ids for pp3_field / pp3_copy_field. */
+enum {
+  PP3_F_STATE = 0,    /* [N][state_stride] f32 */
+  PP3_F_OBS = 1,      /* [N][36H] f32 */
+  PP3_F_REWARD = 2,   /* [N] f32 */
+  PP3_F_DONE = 3,     /* [N] f32 */
+  PP3_F_METRICS = 4,  /* [N][19] f32: total_dist, scaled rewards */
+  PP3_F_DR = 5,       /* [N][62] f32 */
+  PP3_F_PIPELINE = 6, /* [N][PP3_PIPE_STRIDE] f32 (when enabled) */
+  PP3_F_ACTION = 7    /* [N][12] f32 scratch action buffer owned by the handle */
+};
+
+/* Optional pipeline-state output (brax State.x / xd of the last substep,
+ * environment.py:367): written only when pp3_set_pipeline_output(h, 1). */
+enum {
+  PP3_P_XPOS = 0,           /* 13 x 3  body origins (bodies 1..13)       */
+  PP3_P_XQUAT = 39,         /* 13 x 4 */
+  PP3_P_XD_VEL = 91,        /* 13 x 3 */
+  PP3_P_XD_ANG = 130,       /* 13 x 3 */
+  PP3_P_SITE_XPOS = 169,    /*  4 x 3  foot sites                         */
+  PP3_P_QFRC_ACT = 181,     /* 18 */
+  PP3_P_QACC = 199,         /* 18 */
+  PP3_P_NCON = 217,         /*  1  penetrating contacts (float)           */
+  PP3_P_CON_DIST = 218,     /* 16  dist of contacts 0..15                  */
+  PP3_P_CON_GEOM = 234,     /* 32  geom1, geom2 of contacts 0..15 (float)  */
+  PP3_P_SUBTREE_COM = 266,  /*  3 */
+  PP3_PIPE_STRIDE = 272
+};
+
+/* DR record layout (domain_randomization.py:21-66, absolute values). */
+enum {
+  PP3_DR_FRICTION = 0,  /* geom_friction[:,0] for every geom            */
+  PP3_DR_KP = 1,        /* actuator_gainprm[:,0] = -biasprm[:,1]         */
+  PP3_DR_KD = 2,        /* -actuator_biasprm[:,2]                        */
+  PP3_DR_BASE_IPOS = 3, /* body_ipos[1] (3)                               */
+  PP3_DR_INERTIA = 6,   /* body_inertia[14][3]                            */
+  PP3_DR_MASS = 48      /* body_mass[14]                                  */
+};
+
+/* Status codes */
+enum {
+  PP3_OK = 0,
+  PP3_ERR_ARG = 1,
+  PP3_ERR_MODEL = 2,   /* model topology / options unsupported          */
+  PP3_ERR_HIP = 3,
+  PP3_ERR_NOMEM = 4
+};
+
+int pp3_abi_version(void);
+/* sizeof the ABI structs: which = 0 model, 1 env config (ctypes layout check). */
+size_t pp3_struct_size(int which);
+const char* pp3_last_error(void);
+/* HIP device count (0 when no runtime / no GPU). */
+int pp3_device_count(void);
+
+/* Create a batch of `num_envs` environments on `device`.  Validates the model
+ * (replaces the trace-time assert of environment.py:534 and the name lookups of
+ * environment.py:183-203). */
+int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg,
+               int32_t num_envs, int32_t device, pp3_env_t** out);
+int pp3_destroy(pp3_env_t* env);
+int32_t pp3_num_envs(const pp3_env_t* env);
+int32_t pp3_state_stride(const pp3_env_t* env);
+
+/* reset(rng): keys_dev = uint32[N][2] (one jax PRNG key per env); mask_dev =
+ * optional uint8[N] (NULL = all envs).  environment.py:314-346. */
+int pp3_reset(pp3_env_t* env, const uint32_t* keys_dev, const uint8_t* mask_dev, void* stream);
+/* step(state, action): actions_dev = f32[N][12].  environment.py:348-483. */
+int pp3_step(pp3_env_t* env, const float* actions_dev, void* stream);
+/* Per-env DR parameters f32[N][62] (device), or NULL to disable DR. */
+int pp3_set_dr(pp3_env_t* env, const float* dr_dev);
+int pp3_set_pipeline_output(pp3_env_t* env, int32_t enable);
+
+/* Raw physics: `nsteps` x mj_step on the qpos/qvel/qacc_warmstart stored in the
+ * state records, with ctrl_dev = f32[N][12] held fixed (no env logic).  Used by
+ * the substep parity tests; writes the pipeline record of the last substep. */
+int pp3_physics_step(pp3_env_t* env, const float* ctrl_dev, int32_t nsteps, void* stream);
+
+/* Device pointer + element count per env of a field (PP3_F_*). */
+int pp3_field(pp3_env_t* env, int32_t field, void** dev_ptr, int64_t* elems_per_env);
+/* Synchronous host <-> device copies of a whole field (tests / host API). */
+int pp3_copy_field_to_host(pp3_env_t* env, int32_t field, void* host, size_t bytes);
+int pp3_copy_field_from_host(pp3_env_t* env, int32_t field, const void* host, size_t bytes);
+int pp3_synchronize(pp3_env_t* env);
+
+/* Small device-memory helpers so a host can run without any other GPU runtime. */
+int pp3_device_malloc(int32_t device, size_t bytes, void** out);
+int pp3_device_free(void* ptr);
+int pp3_memcpy_h2d(void* dst_dev, const void* src_host, size_t bytes);
+int pp3_memcpy_d2h(void* dst_host, const void* src_dev, size_t bytes);
+int pp3_memcpy_d2d(void* dst_dev, const void* src_dev, size_t bytes, void* stream);
+
+/* Benchmark helpers: fill actions f32[N][12] with U(lo,hi) from a counter hash
+ * keyed by (seed, step) on device; record HIP events around the step kernel
+ * launches on the handle's stream so the average kernel duration can be read. */
+int pp3_fill_uniform(pp3_env_t* env, float* dev, int64_t count, uint32_t seed, uint32_t ctr, float lo, float hi, void* stream);
+int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int32_t nsteps, float* kernel_ms_total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PUPPER_HIP_H_ */

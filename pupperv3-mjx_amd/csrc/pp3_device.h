@@ -1,0 +1,272 @@
+// pp3_device.h -- device-side model layout and small math/RNG helpers for the
+// MI355X (gfx950) Pupper-v3 environment kernels.  fp32 throughout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pupper_hip.h"
+
+namespace pp3 {
+
+constexpr int NB = PP3_NBODY;
+constexpr int NJ = PP3_NJNT;
+constexpr int NV = PP3_NV;
+constexpr int NQ = PP3_NQ;
+constexpr int NU = PP3_NU;
+constexpr int WAVE = 64;
+constexpr int NCMAX = 16;                 // contact cap per env (deepest kept), == oracle ncon_max
+constexpr int NLMAX = 24;                 // joint-limit rows (12 joints x 2 sides)
+constexpr int NFR = 12;                   // frictionloss rows (hinge dofs)
+constexpr int NEFC_MAX = NFR + NLMAX + 4 * NCMAX;
+constexpr int MAX_ROBOT_GEOM = 16;        // collidable geoms on moving bodies
+constexpr int NMPAIR_MAX = 128;           // nonzero (i, j<=i) entries of M
+constexpr float MINVAL = 1e-15f;
+constexpr float MINIMP = 0.0001f;
+constexpr float MAXIMP = 0.9999f;
+
+// fp32 model + env constants, built on the host from pp3_model_t / pp3_env_config_t.
+struct DevModel {
+  // ---- options ----
+  float h;
+  float gravity[3];
+  float impratio;
+  float gtol_scale;  // tolerance * ls_tolerance * meaninertia * nv  (gtol = gtol_scale * |search|)
+  int32_t ls_iterations;
+  int32_t iterations;
+  // ---- bodies ----
+  float body_pos[NB][3];
+  float body_quat[NB][4];
+  float body_iquat[NB][4];
+  float body_ipos[NB][3];
+  float body_mass[NB];
+  float body_inertia[NB][3];
+  uint32_t body_dofmask[NB];  // dofs on the path root..body (ancestor-or-self)
+  int32_t dof_body[NV];
+  // ---- joints (0 = free, 1..12 hinges) ----
+  float jnt_pos[NJ][3];
+  float jnt_axis[NJ][3];
+  float jnt_range[NJ][2];
+  int32_t jnt_limited[NJ];
+  float lim_k[NJ], lim_b[NJ], lim_margin[NJ], lim_invw[NJ];
+  float lim_solimp[NJ][5];  // clamped
+  float qpos0[NQ];
+  // ---- dofs ----
+  float dof_armature[NV];
+  float dof_damping[NV];
+  float fr_floss[NV];  // frictionloss
+  float fr_R[NV];      // R of the frictionloss row (pos = 0 -> imp = dmin)
+  float fr_b[NV];      // damping coefficient of its reference acceleration
+  // ---- mass-matrix sparsity (j ancestor-or-self of i) ----
+  int32_t nmpair;
+  uint8_t mp_i[NMPAIR_MAX], mp_j[NMPAIR_MAX];
+  // ---- collision geoms ----
+  int32_t ncgeom;
+  int32_t cg_type[PP3_MAX_CGEOM];
+  int32_t cg_body[PP3_MAX_CGEOM];
+  int32_t cg_id[PP3_MAX_CGEOM];
+  int32_t cg_slot[PP3_MAX_CGEOM];  // slot in the per-env robot-geom table (-1 = static)
+  float cg_size[PP3_MAX_CGEOM][3];
+  float cg_pos[PP3_MAX_CGEOM][3];      // body frame (robot) or world frame (static)
+  float cg_wmat[PP3_MAX_CGEOM][9];     // world rotation of static geoms
+  int32_t nrobot_geom;
+  int32_t robot_geom[MAX_ROBOT_GEOM];  // cgeom index of each slot
+  int32_t npair;
+  int32_t pair_g1[PP3_MAX_PAIR], pair_g2[PP3_MAX_PAIR];
+  float pair_mu[PP3_MAX_PAIR];
+  float pair_k[PP3_MAX_PAIR], pair_b[PP3_MAX_PAIR];
+  float pair_margin[PP3_MAX_PAIR];
+  float pair_tran[PP3_MAX_PAIR];       // body_invweight0 translational sum
+  float pair_solimp[PP3_MAX_PAIR][5];  // clamped
+  // ---- sites ----
+  int32_t nsite;
+  int32_t site_body[PP3_MAX_SITE];
+  float site_pos[PP3_MAX_SITE][3];
+  // ---- actuators ----
+  int32_t act_dof[NU], act_qadr[NU], act_biastype[NU], act_forcelimited[NU], act_ctrllimited[NU];
+  float act_gear[NU], act_gain[NU], act_bias[NU][3], act_frange[NU][2], act_crange[NU][2];
+  // ---- environment (PupperV3Env kwargs) ----
+  int32_t n_frames, H, La, Li, use_imu, resample_step, term_step;
+  int32_t torso_body;
+  int32_t feet_site[4], lower_leg_body[4];
+  int32_t n_knee_geoms, knee_geoms[16], n_torso_geoms, torso_geoms[8];
+  int32_t partitionable;
+  int32_t stride, imu_off;
+  float lat_dist[PP3_MAX_LAG], imu_lat_dist[PP3_MAX_LAG];
+  float action_scale;
+  float default_pose[NU], jlo[NU], jhi[NU];
+  float des_abd[4];
+  float start_lo[3], start_hi[3];
+  float cmd_x[2], cmd_y[2], cmd_w[2];
+  float zero_cmd_p, stand_thr, max_pitch, max_roll;
+  float n_ang, n_grav, n_motor, n_act;
+  float kick_vel, kick_p;
+  float term_z, cos_term_angle, foot_radius, env_dt, dt;
+  float des_z[3];
+  float scales[PP3_NREWARD];
+  float sigma;
+  float key_qpos[NQ];
+  float pi_f;
+};
+
+// ------------------------------- float helpers -------------------------------
+__device__ __forceinline__ float rlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+__device__ __forceinline__ void quat2mat(const float q[4], float R[9]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void mulquat(float r[4], const float a[4], const float b[4]) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+__device__ __forceinline__ void matvec(float r[3], const float R[9], const float v[3]) {
+  float t0 = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+  float t1 = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+  float t2 = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void cross3(float r[3], const float a[3], const float b[3]) {
+  float t0 = a[1] * b[2] - a[2] * b[1];
+  float t1 = a[2] * b[0] - a[0] * b[2];
+  float t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ float dot3(const float a[3], const float b[3]) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+__device__ __forceinline__ void normalize4(float q[4]) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
+  else { float i = 1.0f / n; q[0] *= i; q[1] *= i; q[2] *= i; q[3] *= i; }
+}
+__device__ __forceinline__ void axisangle2quat(float r[4], const float a[3], float ang) {
+  if (ang == 0.0f) { r[0] = 1; r[1] = r[2] = r[3] = 0; return; }
+  float s, c;
+  sincosf(0.5f * ang, &s, &c);
+  r[0] = c; r[1] = a[0] * s; r[2] = a[1] * s; r[3] = a[2] * s;
+}
+// spatial inertia (10-vector about the root subtree com) times a motion vector
+__device__ __forceinline__ void mul_inert_vec(float r[6], const float* i, const float* v) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+// [w x v_ang ; w x v_lin + vlin x v_ang]
+__device__ __forceinline__ void cross_motion(float r[6], const float* vel, const float* v) {
+  float t0 = -vel[2] * v[1] + vel[1] * v[2];
+  float t1 = vel[2] * v[0] - vel[0] * v[2];
+  float t2 = -vel[1] * v[0] + vel[0] * v[1];
+  float t3 = -vel[2] * v[4] + vel[1] * v[5] - vel[5] * v[1] + vel[4] * v[2];
+  float t4 = vel[2] * v[3] - vel[0] * v[5] + vel[5] * v[0] - vel[3] * v[2];
+  float t5 = -vel[1] * v[3] + vel[0] * v[4] - vel[4] * v[0] + vel[3] * v[1];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3; r[4] = t4; r[5] = t5;
+}
+// [w x f_rot + vlin x f_lin ; w x f_lin]
+__device__ __forceinline__ void cross_force(float r[6], const float* vel, const float* f) {
+  float t0 = -vel[2] * f[1] + vel[1] * f[2] - vel[5] * f[4] + vel[4] * f[5];
+  float t1 = vel[2] * f[0] - vel[0] * f[2] + vel[5] * f[3] - vel[3] * f[5];
+  float t2 = -vel[1] * f[0] + vel[0] * f[1] - vel[4] * f[3] + vel[3] * f[4];
+  float t3 = -vel[2] * f[4] + vel[1] * f[5];
+  float t4 = vel[2] * f[3] - vel[0] * f[5];
+  float t5 = -vel[1] * f[3] + vel[0] * f[4];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3; r[4] = t4; r[5] = t5;
+}
+// brax.math.rotate(v, q) = 2 (u.v) u + (s^2 - u.u) v + 2 s (u x v)
+__device__ __forceinline__ void b_rotate(float r[3], const float v[3], const float q[4]) {
+  float u[3] = {q[1], q[2], q[3]}, c[3];
+  float s = q[0], uv = dot3(u, v), uu = dot3(u, u);
+  cross3(c, u, v);
+  for (int k = 0; k < 3; k++) r[k] = 2 * uv * u[k] + (s * s - uu) * v[k] + 2 * s * c[k];
+}
+
+// MuJoCo impedance (getimpedance), solimp pre-clamped on the host
+__device__ __forceinline__ float getimp(const float* si, float pos, float margin) {
+  float x = fabsf((pos - margin) / si[2]);
+  if (x >= 1.0f) return si[1];
+  if (x <= 0.0f) return si[0];
+  float y;
+  float p = si[4], mid = si[3];
+  if (p == 1.0f) y = x;
+  else if (x <= mid) y = powf(x, p) / powf(mid, p - 1.0f);
+  else y = 1.0f - powf(1.0f - x, p) / powf(1.0f - mid, p - 1.0f);
+  return si[0] + y * (si[1] - si[0]);
+}
+
+// ------------------------------- jax threefry RNG -------------------------------
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ void threefry(uint32_t k0, uint32_t k1, uint32_t x0, uint32_t x1, uint32_t& y0, uint32_t& y1) {
+  const uint32_t k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+  const uint32_t ks[3] = {k0, k1, k2};
+  x0 += k0;
+  x1 += k1;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const int r0 = (i & 1) ? 17 : 13, r1 = (i & 1) ? 29 : 15, r2 = (i & 1) ? 16 : 26, r3 = (i & 1) ? 24 : 6;
+    x0 += x1; x1 = rotl32(x1, r0); x1 ^= x0;
+    x0 += x1; x1 = rotl32(x1, r1); x1 ^= x0;
+    x0 += x1; x1 = rotl32(x1, r2); x1 ^= x0;
+    x0 += x1; x1 = rotl32(x1, r3); x1 ^= x0;
+    x0 += ks[(i + 1) % 3];
+    x1 += ks[(i + 2) % 3] + (uint32_t)(i + 1);
+  }
+  y0 = x0;
+  y1 = x1;
+}
+struct Key { uint32_t a, b; };
+// jax.random.split(key, n)[i]
+__device__ __forceinline__ Key split_i(Key k, int n, int i, int part) {
+  Key r;
+  uint32_t y0, y1;
+  if (part) {
+    threefry(k.a, k.b, 0u, (uint32_t)i, y0, y1);
+    r.a = y0; r.b = y1;
+  } else {
+    int f0 = 2 * i, f1 = 2 * i + 1;
+    threefry(k.a, k.b, (uint32_t)(f0 % n), (uint32_t)(f0 % n + n), y0, y1);
+    r.a = (f0 / n) ? y1 : y0;
+    threefry(k.a, k.b, (uint32_t)(f1 % n), (uint32_t)(f1 % n + n), y0, y1);
+    r.b = (f1 / n) ? y1 : y0;
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t bits_i(Key k, int count, int i, int part) {
+  uint32_t y0, y1;
+  if (part) {
+    threefry(k.a, k.b, 0u, (uint32_t)i, y0, y1);
+    return y0 ^ y1;
+  }
+  int n = count + (count & 1), h = n / 2;
+  int lane = i % h, half = i / h;
+  uint32_t c1 = (lane + h >= count) ? 0u : (uint32_t)(lane + h);
+  threefry(k.a, k.b, (uint32_t)lane, c1, y0, y1);
+  return half ? y1 : y0;
+}
+// jax.random.uniform element i of `count`, float32, no FMA contraction (bit-exact with JAX)
+__device__ __attribute__((noinline)) float uniform_i(Key k, int count, int i, float lo, float hi, int part) {
+#pragma clang fp contract(off)
+  uint32_t b = (bits_i(k, count, i, part) >> 9) | 0x3F800000u;
+  float u = __uint_as_float(b) - 1.0f;
+  float v = u * (hi - lo) + lo;
+  return v > lo ? v : lo;
+}
+
+}  // namespace pp3

@@ -1,0 +1,114 @@
+"""ctypes binding of the C-ABI in include/pupper_hip.h (libpupper_hip.so, built in-tree).
+
+This is the binding a maintainer adds on the reference side.  There is
+no fallback: if the HIP library is missing or no GPU is visible, the product path raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpupper_hip.so")
+_lib = None
+
+
+class PupperHipError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PupperHipError(
+            f"HIP extension not built: {LIB_PATH} is missing (run __graft_entry__.build() or make -C "
+            "pupperv3-mjx_amd/csrc); there is no CPU fallback for the environment step.")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_size_t
+    L.pp3_abi_version.restype = C.c_int
+    L.pp3_struct_size.argtypes = [C.c_int]
+    L.pp3_struct_size.restype = sz
+    L.pp3_last_error.restype = C.c_char_p
+    L.pp3_device_count.restype = C.c_int
+    L.pp3_create.argtypes = [C.POINTER(_abi.Model), C.POINTER(_abi.EnvConfig), i32, i32, C.POINTER(vp)]
+    L.pp3_destroy.argtypes = [vp]
+    L.pp3_num_envs.argtypes = [vp]
+    L.pp3_num_envs.restype = i32
+    L.pp3_state_stride.argtypes = [vp]
+    L.pp3_state_stride.restype = i32
+    L.pp3_reset.argtypes = [vp, vp, vp, vp]
+    L.pp3_step.argtypes = [vp, vp, vp]
+    L.pp3_set_dr.argtypes = [vp, vp]
+    L.pp3_set_pipeline_output.argtypes = [vp, i32]
+    L.pp3_physics_step.argtypes = [vp, vp, i32, vp]
+    L.pp3_field.argtypes = [vp, i32, C.POINTER(vp), C.POINTER(i64)]
+    L.pp3_copy_field_to_host.argtypes = [vp, i32, vp, sz]
+    L.pp3_copy_field_from_host.argtypes = [vp, i32, vp, sz]
+    L.pp3_synchronize.argtypes = [vp]
+    L.pp3_device_malloc.argtypes = [i32, sz, C.POINTER(vp)]
+    L.pp3_device_free.argtypes = [vp]
+    L.pp3_memcpy_h2d.argtypes = [vp, vp, sz]
+    L.pp3_memcpy_d2h.argtypes = [vp, vp, sz]
+    L.pp3_memcpy_d2d.argtypes = [vp, vp, sz, vp]
+    L.pp3_fill_uniform.argtypes = [vp, vp, i64, C.c_uint32, C.c_uint32, C.c_float, C.c_float, vp]
+    L.pp3_step_timed.argtypes = [vp, vp, i32, C.POINTER(C.c_float)]
+    for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
+                 "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
+                 "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
+                 "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed"):
+        getattr(L, name).restype = C.c_int
+    if L.pp3_abi_version() != _abi.ABI_VERSION:
+        raise PupperHipError("ABI version mismatch between libpupper_hip.so and pupperv3_mjx/_abi.py")
+    if L.pp3_struct_size(0) != C.sizeof(_abi.Model) or L.pp3_struct_size(1) != C.sizeof(_abi.EnvConfig):
+        raise PupperHipError("struct layout mismatch between include/pupper_hip.h and pupperv3_mjx/_abi.py")
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().pp3_last_error().decode(errors="replace")
+        raise PupperHipError(f"pupper_hip error {rc}: {msg}")
+
+
+EXPORTED_SYMBOLS = (
+    "pp3_abi_version", "pp3_struct_size", "pp3_last_error", "pp3_device_count", "pp3_create", "pp3_destroy",
+    "pp3_num_envs", "pp3_state_stride", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
+    "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
+    "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
+    "pp3_fill_uniform", "pp3_step_timed",
+)
+
+
+class DeviceBuffer:
+    """Minimal owning device allocation (no torch needed)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        L = load()
+        self.ptr = C.c_void_p()
+        self.nbytes = int(nbytes)
+        check(L.pp3_device_malloc(device, max(self.nbytes, 4), C.byref(self.ptr)))
+
+    def upload(self, arr) -> None:
+        import numpy as np
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        check(load().pp3_memcpy_h2d(self.ptr, a.ctypes.data_as(C.c_void_p), a.nbytes))
+
+    def download(self, arr) -> None:
+        check(load().pp3_memcpy_d2h(arr.ctypes.data_as(C.c_void_p), self.ptr, arr.nbytes))
+
+    def free(self) -> None:
+        if self.ptr:
+            load().pp3_device_free(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

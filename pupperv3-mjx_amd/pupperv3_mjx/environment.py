@@ -1,0 +1,462 @@
+"""PupperV3Env: the reference's environment surface over the MI355X HIP kernels.
+
+Same constructor knobs and defaults as environment.py:35-121, same reset/step/observation/
+reward semantics (environment.py:314-543, rewards.py), executed by the fused HIP kernels in
+csrc/pp3_env.hip through the C-ABI (include/pupper_hip.h).  Differences in *form* (not in
+numbers), all forced by the device-resident design:
+
+* the env is batched: ``PupperV3Env(..., num_envs=N)``; ``reset(rng)`` takes N keys [N, 2]
+  (or one key [2] when N == 1) and ``step(state, action)`` takes actions [N, 12];
+* ``State`` fields are numpy host copies (``obs`` [N, 36H], ``reward`` [N], ``done`` [N],
+  ``metrics``/``info`` dicts of [N, ...] arrays); ``step`` packs ``state.info`` / qpos / qvel
+  back into the device record first, so editing ``state.info["command"]`` works as in
+  test_environment.py:291;
+* the zero-copy path for training loops is ``step_device`` / ``device_fields`` (no host
+  round trip); ``State.pipeline_state`` exposes q, qd, x, xd, site_xpos, qfrc_actuator and
+  contacts of the last substep (brax State semantics, environment.py:367).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _abi, _lib, domain_randomization, mjcf
+from . import rng as _rng
+
+
+@dataclass
+class Transform:
+    pos: np.ndarray
+    rot: np.ndarray
+
+
+@dataclass
+class Motion:
+    vel: np.ndarray
+    ang: np.ndarray
+
+
+@dataclass
+class Contact:
+    dist: np.ndarray
+    geom1: np.ndarray
+    geom2: np.ndarray
+
+
+@dataclass
+class PipelineState:
+    q: np.ndarray
+    qd: np.ndarray
+    qacc_warmstart: np.ndarray
+    x: Optional[Transform] = None
+    xd: Optional[Motion] = None
+    site_xpos: Optional[np.ndarray] = None
+    qfrc_actuator: Optional[np.ndarray] = None
+    qacc: Optional[np.ndarray] = None
+    contact: Optional[Contact] = None
+    subtree_com: Optional[np.ndarray] = None
+
+    @property
+    def qpos(self):
+        return self.q
+
+    @property
+    def qvel(self):
+        return self.qd
+
+
+@dataclass
+class State:
+    pipeline_state: PipelineState
+    obs: np.ndarray
+    reward: np.ndarray
+    done: np.ndarray
+    metrics: Dict[str, np.ndarray] = field(default_factory=dict)
+    info: Dict[str, Any] = field(default_factory=dict)
+
+
+_DEFAULT_LOWER = [-1.220, -0.420, -2.790, -2.510, -3.140, -0.710, -1.220, -0.420, -2.790, -2.510, -3.140, -0.710]
+_DEFAULT_UPPER = [2.510, 3.140, 0.710, 1.220, 0.420, 2.790, 2.510, 3.140, 0.710, 1.220, 0.420, 2.790]
+_DEFAULT_POSE = [0.26, 0.0, -0.52, -0.26, 0.0, 0.52, 0.26, 0.0, -0.52, -0.26, 0.0, 0.52]
+
+
+class PupperV3Env:
+    """Environment for training the Pupper V3 joystick policy on MI355X."""
+
+    def __init__(
+        self,
+        path: str,
+        reward_config: Dict,
+        action_scale: float,
+        observation_history: int,
+        joint_lower_limits: Sequence = tuple(_DEFAULT_LOWER),
+        joint_upper_limits: Sequence = tuple(_DEFAULT_UPPER),
+        dof_damping: float = 0.25,
+        position_control_kp: float = 5.0,
+        start_position_config: domain_randomization.StartPositionRandomization = (
+            domain_randomization.StartPositionRandomization(
+                x_min=-2.0, x_max=2.0, y_min=-2.0, y_max=2.0, z_min=0.15, z_max=0.20)),
+        foot_site_names: Sequence[str] = ("leg_front_r_3_foot_site", "leg_front_l_3_foot_site",
+                                          "leg_back_r_3_foot_site", "leg_back_l_3_foot_site"),
+        torso_name: str = "base_link",
+        upper_leg_body_names: Sequence[str] = ("leg_front_r_2", "leg_front_l_2", "leg_back_r_2", "leg_back_l_2"),
+        lower_leg_body_names: Sequence[str] = ("leg_front_r_3", "leg_front_l_3", "leg_back_r_3", "leg_back_l_3"),
+        resample_velocity_step: int = 500,
+        linear_velocity_x_range: Tuple[float, float] = (-0.75, 0.75),
+        linear_velocity_y_range: Tuple[float, float] = (-0.5, 0.5),
+        angular_velocity_range: Tuple[float, float] = (-2.0, 2.0),
+        zero_command_probability: float = 0.01,
+        stand_still_command_threshold: float = 0.1,
+        maximum_pitch_command: float = 0.0,
+        maximum_roll_command: float = 0.0,
+        default_pose: Sequence = tuple(_DEFAULT_POSE),
+        desired_abduction_angles: Sequence = (0.0, 0.0, 0.0, 0.0),
+        angular_velocity_noise: float = 0.3,
+        gravity_noise: float = 0.1,
+        motor_angle_noise: float = 0.1,
+        last_action_noise: float = 0.01,
+        kick_vel: float = 0.2,
+        kick_probability: float = 0.02,
+        terminal_body_z: float = 0.1,
+        early_termination_step_threshold: int = 500,
+        terminal_body_angle: float = 0.52,
+        foot_radius: float = 0.02,
+        environment_timestep: float = 0.02,
+        physics_timestep: float = 0.004,
+        latency_distribution: Sequence = (0.2, 0.8),
+        imu_latency_distribution: Sequence = (0.5, 0.5),
+        desired_world_z_in_body_frame: Sequence = (0.0, 0.0, 1.0),
+        use_imu: bool = True,
+        *,
+        num_envs: int = 1,
+        device: int = 0,
+        rng_partitionable: bool = True,
+        pipeline_output: bool = True,
+        create_device: bool = True,
+    ):
+        cm = mjcf.load(path)
+        m = cm.struct
+        # environment.py:165-180: dt override, PD gains, home keyframe, n_frames
+        m.timestep = float(physics_timestep)
+        for i in range(_abi.NU):
+            m.actuator_gainprm[i][0] = position_control_kp
+            m.actuator_biasprm[i][1] = -position_control_kp
+            m.actuator_biasprm[i][2] = -dof_damping
+        default_pose = np.asarray(default_pose, dtype=np.float64)
+        m.key_qpos[7:] = list(default_pose)
+        n_frames = int(environment_timestep // m.timestep)
+        self.sys_model = cm
+        self._dt = environment_timestep
+        self._n_frames = n_frames
+        self._reward_config = reward_config
+        self._torso_idx = cm.body_id(torso_name)
+        assert self._torso_idx != -1, "torso not found"
+        self._torso_geom_ids = cm.body_geom_ids(torso_name)
+        feet = [cm.site_id(f) for f in foot_site_names]
+        assert not any(i == -1 for i in feet), "Site not found."
+        self._feet_site_id = np.array(feet)
+        lower = [cm.body_id(n) for n in lower_leg_body_names]
+        assert not any(i == -1 for i in lower), "Body not found."
+        self._lower_leg_body_id = np.array(lower)
+        self._upper_leg_geom_ids = np.concatenate([cm.body_geom_ids(n) for n in upper_leg_body_names])
+        self._default_pose = default_pose
+        self._action_scale = float(action_scale)
+        self._observation_history = int(observation_history)
+        self.observation_dim = _abi.OBS_DIM
+        self.lowers = np.asarray(joint_lower_limits, dtype=np.float64)
+        self.uppers = np.asarray(joint_upper_limits, dtype=np.float64)
+        self._latency_distribution = np.asarray(latency_distribution, dtype=np.float32)
+        self._imu_latency_distribution = np.asarray(imu_latency_distribution, dtype=np.float32)
+        self._use_imu = bool(use_imu)
+        self._partitionable = bool(rng_partitionable)
+        self.num_envs = int(num_envs)
+        self.device = int(device)
+
+        c = _abi.EnvConfig()
+        c.n_frames = n_frames
+        c.obs_history = self._observation_history
+        c.use_imu = int(use_imu)
+        c.latency_len = len(self._latency_distribution)
+        c.imu_latency_len = len(self._imu_latency_distribution)
+        c.resample_velocity_step = int(resample_velocity_step)
+        c.early_termination_step_threshold = int(early_termination_step_threshold)
+        c.torso_body = self._torso_idx
+        c.feet_site[:] = [int(v) for v in feet]
+        c.lower_leg_body[:] = [int(v) for v in lower]
+        ul = [int(v) for v in self._upper_leg_geom_ids]
+        c.n_upper_leg_geoms = len(ul)
+        c.upper_leg_geoms[:len(ul)] = ul
+        tg = [int(v) for v in self._torso_geom_ids]
+        c.n_torso_geoms = len(tg)
+        c.torso_geoms[:len(tg)] = tg
+        c.rng_partitionable = int(rng_partitionable)
+        c.latency_dist[:c.latency_len] = [float(v) for v in self._latency_distribution]
+        c.imu_latency_dist[:c.imu_latency_len] = [float(v) for v in self._imu_latency_distribution]
+        c.action_scale = float(action_scale)
+        c.default_pose[:] = list(default_pose)
+        c.joint_lower[:] = [float(v) for v in self.lowers]
+        c.joint_upper[:] = [float(v) for v in self.uppers]
+        c.desired_abduction[:] = [float(v) for v in desired_abduction_angles]
+        sp = start_position_config
+        c.start_pos_min[:] = [sp.x_min, sp.y_min, sp.z_min]
+        c.start_pos_max[:] = [sp.x_max, sp.y_max, sp.z_max]
+        c.lin_vel_x_range[:] = list(linear_velocity_x_range)
+        c.lin_vel_y_range[:] = list(linear_velocity_y_range)
+        c.ang_vel_range[:] = list(angular_velocity_range)
+        c.zero_command_probability = zero_command_probability
+        c.stand_still_command_threshold = stand_still_command_threshold
+        c.max_pitch_command = maximum_pitch_command
+        c.max_roll_command = maximum_roll_command
+        c.ang_vel_noise = angular_velocity_noise
+        c.gravity_noise = gravity_noise
+        c.motor_angle_noise = motor_angle_noise
+        c.last_action_noise = last_action_noise
+        c.kick_vel = kick_vel
+        c.kick_probability = kick_probability
+        c.terminal_body_z = terminal_body_z
+        c.terminal_body_angle = terminal_body_angle
+        c.foot_radius = foot_radius
+        c.env_dt = environment_timestep
+        c.dt = m.timestep * n_frames
+        c.desired_world_z[:] = [float(v) for v in desired_world_z_in_body_frame]
+        scales = reward_config.rewards.scales
+        c.reward_scales[:] = [float(scales[k]) for k in _abi.REWARD_NAMES]
+        c.tracking_sigma = float(reward_config.rewards.tracking_sigma)
+        self.config_struct = c
+        self._reward_keys = list(scales.keys())
+        self._sys = domain_randomization.System(
+            geom_friction=cm.geom_friction.copy(),
+            actuator_gainprm=np.pad(np.array(m.actuator_gainprm[:], dtype=np.float64), ((0, 0), (0, 7))),
+            actuator_biasprm=np.pad(np.array(m.actuator_biasprm[:], dtype=np.float64), ((0, 0), (0, 7))),
+            body_ipos=np.array(m.body_ipos[:], dtype=np.float64),
+            body_inertia=np.array(m.body_inertia[:], dtype=np.float64),
+            body_mass=np.array(m.body_mass[:], dtype=np.float64),
+        )
+        self._h = None
+        self.stride = _abi.state_stride(c.latency_len, c.imu_latency_len)
+        self._pipeline_output = bool(pipeline_output)
+        if not create_device:  # host-only construction (tests/oracle tooling): structs, no GPU
+            return
+
+        L = _lib.load()
+        h = C.c_void_p()
+        _lib.check(L.pp3_create(C.byref(m), C.byref(c), self.num_envs, self.device, C.byref(h)))
+        self._h = h
+        self._L = L
+        assert int(L.pp3_state_stride(h)) == self.stride
+        _lib.check(L.pp3_set_pipeline_output(h, int(pipeline_output)))
+        self._keys_buf = _lib.DeviceBuffer(self.num_envs * 8, self.device)
+        self._act_buf = _lib.DeviceBuffer(self.num_envs * _abi.NU * 4, self.device)
+        self._dr_buf = None
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def dt(self) -> float:
+        return self.sys_model.struct.timestep * self._n_frames
+
+    @property
+    def observation_size(self) -> int:
+        return self.observation_dim * self._observation_history
+
+    @property
+    def action_size(self) -> int:
+        return _abi.NU
+
+    @property
+    def sys(self) -> domain_randomization.System:
+        return self._sys
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.pp3_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ DR
+    def set_domain_randomization(self, sys_batched: Optional[domain_randomization.System]) -> None:
+        """Upload the per-env parameters of a batched System (or None to disable DR)."""
+        if sys_batched is None:
+            _lib.check(self._L.pp3_set_dr(self._h, None))
+            return
+        table = np.ascontiguousarray(sys_batched.dr_table(), dtype=np.float32)
+        if table.shape[0] != self.num_envs:
+            raise ValueError("DR batch size must equal num_envs")
+        _lib.check(self._L.pp3_copy_field_from_host(self._h, _abi.F_DR, table.ctypes.data_as(C.c_void_p), table.nbytes))
+
+    # ------------------------------------------------------------------ device API
+    def device_field(self, field_id: int) -> Tuple[int, int]:
+        """(device pointer, elements per env) of a PP3_F_* buffer."""
+        p = C.c_void_p()
+        n = C.c_int64()
+        _lib.check(self._L.pp3_field(self._h, field_id, C.byref(p), C.byref(n)))
+        return p.value, n.value
+
+    def reset_device(self, keys_dev: int, mask_dev: Optional[int] = None, stream: Optional[int] = None) -> None:
+        _lib.check(self._L.pp3_reset(self._h, C.c_void_p(keys_dev), C.c_void_p(mask_dev) if mask_dev else None,
+                                     C.c_void_p(stream) if stream else None))
+
+    def step_device(self, actions_dev: int, stream: Optional[int] = None) -> None:
+        _lib.check(self._L.pp3_step(self._h, C.c_void_p(actions_dev), C.c_void_p(stream) if stream else None))
+
+    def synchronize(self) -> None:
+        _lib.check(self._L.pp3_synchronize(self._h))
+
+    def _get(self, field_id: int, dtype=np.float32) -> np.ndarray:
+        _, n = self.device_field(field_id)
+        out = np.empty((self.num_envs, n), dtype=np.float32)
+        _lib.check(self._L.pp3_copy_field_to_host(self._h, field_id, out.ctypes.data_as(C.c_void_p), out.nbytes))
+        return out
+
+    def _put(self, field_id: int, arr: np.ndarray) -> None:
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        _lib.check(self._L.pp3_copy_field_from_host(self._h, field_id, a.ctypes.data_as(C.c_void_p), a.nbytes))
+
+    # ------------------------------------------------------------------ host API
+    def _batch_keys(self, rng) -> Tuple[np.ndarray, bool]:
+        k = np.asarray(rng, dtype=np.uint32)
+        single = k.ndim == 1
+        k = k.reshape(-1, 2)
+        if k.shape[0] != self.num_envs:
+            raise ValueError(f"reset expects {self.num_envs} keys, got {k.shape[0]}")
+        return np.ascontiguousarray(k), single
+
+    def reset(self, rng) -> State:
+        keys, single = self._batch_keys(rng)
+        self._keys_buf.upload(keys)
+        self.reset_device(self._keys_buf.ptr.value)
+        self.synchronize()
+        return self._read_state(single)
+
+    def step(self, state: State, action) -> State:
+        single = np.ndim(state.reward) == 0
+        act = np.ascontiguousarray(np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU))
+        self._write_state(state)
+        self._act_buf.upload(act)
+        self.step_device(self._act_buf.ptr.value)
+        self.synchronize()
+        return self._read_state(single)
+
+    # ------------------------------------------------------------------ packing
+    def _unpack_info(self, rec: np.ndarray) -> Dict[str, Any]:
+        La = len(self._latency_distribution)
+        Li = len(self._imu_latency_distribution)
+        io = _abi.imu_buf_offset(La)
+        info = {
+            "rng": rec[:, _abi.S_RNG:_abi.S_RNG + 2].copy().view(np.uint32),
+            "last_act": rec[:, _abi.S_LAST_ACT:_abi.S_LAST_ACT + 12].copy(),
+            "action_buffer": rec[:, _abi.S_ACT_BUF:_abi.S_ACT_BUF + 12 * La].reshape(-1, 12, La).copy(),
+            "imu_buffer": rec[:, io:io + 6 * Li].reshape(-1, 6, Li).copy(),
+            "last_vel": rec[:, _abi.S_LAST_VEL:_abi.S_LAST_VEL + 12].copy(),
+            "command": rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3].copy(),
+            "last_contact": rec[:, _abi.S_LAST_CONTACT:_abi.S_LAST_CONTACT + 4] != 0,
+            "feet_air_time": rec[:, _abi.S_AIR_TIME:_abi.S_AIR_TIME + 4].copy(),
+            "kick": rec[:, _abi.S_KICK:_abi.S_KICK + 2].copy(),
+            "step": rec[:, _abi.S_STEP].astype(np.int32),
+            "desired_world_z_in_body_frame": rec[:, _abi.S_DESIRED_Z:_abi.S_DESIRED_Z + 3].copy(),
+        }
+        return info
+
+    def _read_state(self, single: bool) -> State:
+        rec = self._get(_abi.F_STATE)
+        obs = self._get(_abi.F_OBS)
+        rew = self._get(_abi.F_REWARD)[:, 0]
+        done = self._get(_abi.F_DONE)[:, 0]
+        met = self._get(_abi.F_METRICS)
+        info = self._unpack_info(rec)
+        info["rewards"] = {k: met[:, 1 + i] for i, k in enumerate(_abi.REWARD_NAMES)}
+        metrics = {"total_dist": met[:, 0]}
+        metrics.update(info["rewards"])
+        ps = PipelineState(q=rec[:, _abi.S_QPOS:_abi.S_QPOS + 19].copy(), qd=rec[:, _abi.S_QVEL:_abi.S_QVEL + 18].copy(),
+                           qacc_warmstart=rec[:, _abi.S_QACC_WS:_abi.S_QACC_WS + 18].copy())
+        if self._pipeline_output:
+            p = self._get(_abi.F_PIPELINE)
+            nb = _abi.NBODY - 1
+            ps.x = Transform(pos=p[:, _abi.P_XPOS:_abi.P_XPOS + 3 * nb].reshape(-1, nb, 3),
+                             rot=p[:, _abi.P_XQUAT:_abi.P_XQUAT + 4 * nb].reshape(-1, nb, 4))
+            ps.xd = Motion(vel=p[:, _abi.P_XD_VEL:_abi.P_XD_VEL + 3 * nb].reshape(-1, nb, 3),
+                           ang=p[:, _abi.P_XD_ANG:_abi.P_XD_ANG + 3 * nb].reshape(-1, nb, 3))
+            ps.site_xpos = p[:, _abi.P_SITE_XPOS:_abi.P_SITE_XPOS + 12].reshape(-1, 4, 3)
+            ps.qfrc_actuator = p[:, _abi.P_QFRC_ACT:_abi.P_QFRC_ACT + 18]
+            ps.qacc = p[:, _abi.P_QACC:_abi.P_QACC + 18]
+            ncon = p[:, _abi.P_NCON].astype(np.int32)
+            g = p[:, _abi.P_CON_GEOM:_abi.P_CON_GEOM + 32].reshape(-1, 16, 2).astype(np.int32)
+            ps.contact = Contact(dist=p[:, _abi.P_CON_DIST:_abi.P_CON_DIST + 16], geom1=g[..., 0], geom2=g[..., 1])
+            ps.contact.ncon = ncon
+            ps.subtree_com = p[:, _abi.P_SUBTREE_COM:_abi.P_SUBTREE_COM + 3]
+        st = State(pipeline_state=ps, obs=obs, reward=rew, done=done, metrics=metrics, info=info)
+        st._record = rec
+        if single:
+            st = _squeeze(st)
+        return st
+
+    def _write_state(self, state: State) -> None:
+        rec = getattr(state, "_record", None)
+        if rec is None:
+            raise ValueError("state must come from this env's reset/step")
+        rec = rec.copy()
+        info = state.info
+        ps = state.pipeline_state
+        La = len(self._latency_distribution)
+        Li = len(self._imu_latency_distribution)
+        io = _abi.imu_buf_offset(La)
+        n = self.num_envs
+
+        def put(off, val, width):
+            rec[:, off:off + width] = np.asarray(val, dtype=np.float32).reshape(n, width)
+
+        put(_abi.S_QPOS, ps.q, 19)
+        put(_abi.S_QVEL, ps.qd, 18)
+        put(_abi.S_QACC_WS, ps.qacc_warmstart, 18)
+        rec[:, _abi.S_RNG:_abi.S_RNG + 2] = np.asarray(info["rng"], dtype=np.uint32).reshape(n, 2).view(np.float32)
+        put(_abi.S_LAST_ACT, info["last_act"], 12)
+        put(_abi.S_LAST_VEL, info["last_vel"], 12)
+        put(_abi.S_COMMAND, info["command"], 3)
+        put(_abi.S_DESIRED_Z, info["desired_world_z_in_body_frame"], 3)
+        put(_abi.S_AIR_TIME, info["feet_air_time"], 4)
+        put(_abi.S_LAST_CONTACT, np.asarray(info["last_contact"], dtype=np.float32), 4)
+        put(_abi.S_KICK, info["kick"], 2)
+        put(_abi.S_STEP, np.asarray(info["step"], dtype=np.float32), 1)
+        put(_abi.S_ACT_BUF, info["action_buffer"], 12 * La)
+        put(io, info["imu_buffer"], 6 * Li)
+        self._put(_abi.F_STATE, rec)
+        self._put(_abi.F_OBS, np.asarray(state.obs, dtype=np.float32).reshape(n, -1))
+
+
+def _squeeze(st: State) -> State:
+    """Drop the leading batch axis of a 1-env State (single-key reset API)."""
+
+    def sq(v):
+        if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == 1:
+            return v[0]
+        if isinstance(v, dict):
+            return {k: sq(x) for k, x in v.items()}
+        return v
+
+    ps = st.pipeline_state
+    ps2 = PipelineState(q=sq(ps.q), qd=sq(ps.qd), qacc_warmstart=sq(ps.qacc_warmstart))
+    if ps.x is not None:
+        ps2.x = Transform(sq(ps.x.pos), sq(ps.x.rot))
+        ps2.xd = Motion(sq(ps.xd.vel), sq(ps.xd.ang))
+        ps2.site_xpos = sq(ps.site_xpos)
+        ps2.qfrc_actuator = sq(ps.qfrc_actuator)
+        ps2.qacc = sq(ps.qacc)
+        ps2.contact = Contact(sq(ps.contact.dist), sq(ps.contact.geom1), sq(ps.contact.geom2))
+        ps2.subtree_com = sq(ps.subtree_com)
+    out = State(pipeline_state=ps2, obs=sq(st.obs), reward=sq(st.reward), done=sq(st.done),
+                metrics=sq(st.metrics), info=sq(st.info))
+    out._record = st._record
+    return out
+
+
+def make_keys(seed: int, n: int, partitionable: bool = True) -> np.ndarray:
+    """N per-env reset keys = jax.random.split(PRNGKey(seed), N)."""
+    return _rng.split(_rng.PRNGKey(seed), n, partitionable)

@@ -1,0 +1,66 @@
+"""Static obstacle boxes ("rails") added to the MJCF worldbody.
+
+Behavioural mirror of obstacles.py:16-57: the stdlib Mersenne-Twister ``random`` module is
+seeded once with ``seed`` and, per box, draws x, y and a yaw in that order, so a given seed
+produces the same boxes (pinned against a fixture generated from the reference module in
+tests/golden/obstacles_seed0.json).  Boxes are static world geoms shared by all envs; the
+HIP kernel collides every robot sphere against each of them (sphere-box narrow phase).
+"""
+from __future__ import annotations
+
+import math
+import random
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+
+@dataclass
+class BoxSpec:
+    name: str
+    x: float
+    y: float
+    quat: Tuple[float, int, int, float]
+    half_sizes: Tuple[float, float, float]
+
+
+def random_z_rotation_quaternion(seed: int = 0):
+    """(w, 0, 0, z) for a yaw drawn uniformly in [-pi, pi] from the global `random` stream.
+
+    As in the reference, `seed` is accepted but not used (the stream is seeded by the caller).
+    """
+    half = random.uniform(-math.pi, math.pi) / 2
+    return [math.cos(half), 0, 0, math.sin(half)]
+
+
+def sample_boxes(n_boxes: int, x_range: Sequence[float], y_range: Sequence[float], height: float = 0.02,
+                 depth: float = 0.02, length: float = 3.0, seed: int = 0) -> List[BoxSpec]:
+    random.seed(seed)
+    specs = []
+    for i in range(n_boxes):
+        x = random.uniform(x_range[0], x_range[1])
+        y = random.uniform(y_range[0], y_range[1])
+        q = random_z_rotation_quaternion(seed=seed)
+        specs.append(BoxSpec(f"box_geom_{i}", x, y, tuple(q), (depth / 2.0, length / 2.0, height)))
+    return specs
+
+
+def add_boxes_to_model(tree: ET.ElementTree, n_boxes: int, x_range: Tuple, y_range: Tuple, height: float = 0.02,
+                       depth: float = 0.02, length: float = 3.0, group: str = "0", seed: int = 0) -> ET.ElementTree:
+    """Append `n_boxes` box geoms to <worldbody>; returns the (mutated) tree."""
+    world = tree.getroot().find("worldbody")
+    for b in sample_boxes(n_boxes, x_range, y_range, height, depth, length, seed):
+        attrs = {
+            "name": b.name,
+            "pos": f"{b.x} {b.y} 0",
+            "quat": " ".join(str(v) for v in b.quat),
+            "type": "box",
+            "size": " ".join(str(v) for v in b.half_sizes),
+            "rgba": "0.1 0.5 0.8 1",
+            "conaffinity": "1",
+            "contype": "1",
+            "condim": "3",
+            "group": group,
+        }
+        ET.SubElement(world, "geom", attrs)
+    return tree

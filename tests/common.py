@@ -1,0 +1,96 @@
+"""Shared builders: the reference test fixture's env kwargs (test_environment.py:64-113)."""
+import copy
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+from pupperv3_mjx import MODEL_XML, _abi, config, domain_randomization, mjcf, obstacles
+
+DEFAULT_POSE = [0.26, 0.0, -0.52, -0.26, 0.0, 0.52, 0.26, 0.0, -0.52, -0.26, 0.0, 0.52]
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def model_with_obstacles_xml(n=10):
+    tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
+    obstacles.add_boxes_to_model(tree, n_boxes=n, x_range=(-5, 5), y_range=(-5, 5), height=0.02, length=6.0)
+    return ET.tostring(tree.getroot(), encoding="unicode")
+
+
+def write_model(tmp_path, obstacles_n=0):
+    if obstacles_n:
+        xml = model_with_obstacles_xml(obstacles_n)
+    else:
+        xml = open(MODEL_XML).read()
+    p = os.path.join(str(tmp_path), f"model_{obstacles_n}.xml")
+    with open(p, "w") as f:
+        f.write(xml)
+    return p
+
+
+def fixture_kwargs(path, **over):
+    """test_environment.py:64-113 env kwargs (joint limits taken from the model's jnt_range)."""
+    cm = mjcf.load(path)
+    kw = dict(
+        path=path, action_scale=0.75, observation_history=2,
+        joint_lower_limits=list(cm.jnt_range[1:, 0]), joint_upper_limits=list(cm.jnt_range[1:, 1]),
+        dof_damping=0.25, position_control_kp=5.0,
+        foot_site_names=["leg_front_r_3_foot_site", "leg_front_l_3_foot_site", "leg_back_r_3_foot_site",
+                         "leg_back_l_3_foot_site"],
+        torso_name="base_link",
+        upper_leg_body_names=["leg_front_r_2", "leg_front_l_2", "leg_back_r_2", "leg_back_l_2"],
+        lower_leg_body_names=["leg_front_r_3", "leg_front_l_3", "leg_back_r_3", "leg_back_l_3"],
+        resample_velocity_step=100, linear_velocity_x_range=[-0.75, 0.75], linear_velocity_y_range=[-0.5, 0.5],
+        angular_velocity_range=[-2.0, 2.0], maximum_pitch_command=30, maximum_roll_command=30,
+        default_pose=DEFAULT_POSE,
+        start_position_config=domain_randomization.StartPositionRandomization(
+            x_min=-1.0, x_max=1.0, y_min=-1.0, y_max=1.0, z_min=0.18, z_max=0.24),
+        reward_config=config.get_config(), kick_vel=1.0, kick_probability=0.04, terminal_body_z=0.1,
+        early_termination_step_threshold=500,
+    )
+    kw.update(over)
+    return kw
+
+
+def env_model_and_config(path, **over):
+    """(model struct, env config struct, host-only env) built exactly as PupperV3Env.__init__ does."""
+    from pupperv3_mjx.environment import PupperV3Env
+    env = PupperV3Env(**fixture_kwargs(path, **over), create_device=False)
+    return env.sys_model.struct, env.config_struct, env
+
+
+def pd_model(path=None):
+    """Model with the env's PD overrides (Kp=5, Kd=0.25) and dt=0.004."""
+    cm = mjcf.load(path or MODEL_XML)
+    m = cm.struct
+    m.timestep = 0.004
+    for i in range(12):
+        m.actuator_gainprm[i][0] = 5.0
+        m.actuator_biasprm[i][1] = -5.0
+        m.actuator_biasprm[i][2] = -0.25
+    return cm
+
+
+def random_physics_states(n, seed=0, mode="mixed"):
+    """Seeded initial (qpos, qvel, qacc_ws, ctrl) covering air, standing and contact-rich cases."""
+    rs = np.random.RandomState(seed)
+    qpos = np.zeros((n, 19))
+    qvel = np.zeros((n, 18))
+    ctrl = np.zeros((n, 12))
+    for i in range(n):
+        kind = mode if mode != "mixed" else ("air", "stand", "low", "tilt")[i % 4]
+        yaw = rs.uniform(-np.pi, np.pi)
+        q = np.array([np.cos(yaw / 2), 0, 0, np.sin(yaw / 2)])
+        z = {"air": 0.5, "stand": 0.155, "low": 0.12, "tilt": 0.16}[kind]
+        if kind == "tilt":
+            ax = rs.normal(size=3)
+            ax /= np.linalg.norm(ax)
+            ang = rs.uniform(0.2, 0.8)
+            dq = np.concatenate([[np.cos(ang / 2)], ax * np.sin(ang / 2)])
+            q = mjcf.quat_mul(q, dq)
+        qpos[i, :3] = [rs.uniform(-1, 1), rs.uniform(-1, 1), z]
+        qpos[i, 3:7] = q
+        qpos[i, 7:] = np.array(DEFAULT_POSE) + rs.uniform(-0.3, 0.3, 12)
+        qvel[i] = rs.normal(scale=0.3, size=18)
+        ctrl[i] = np.array(DEFAULT_POSE) + rs.uniform(-0.5, 0.5, 12)
+    return qpos, qvel, np.zeros((n, 18)), ctrl
