@@ -1282,18 +1282,18 @@ static void sample_orientation(const Env* e, key_t2 rng, real out[3]) {
 }
 
 /* _get_obs (environment.py:485-543): consumes state rng, pushes the IMU buffer, rolls history */
-static void get_obs(const Env* e, const Data* d, real* st, real* obs) {
+static void get_obs(const Env* e, const Data* d, real* st, uint32_t* rngw, real* obs) {
   const pp3_env_config_t* c = &e->c;
   real inv[4] = {1, 0, 0, 0}, angl[3] = {0, 0, 0};
   if (c->use_imu) {
     b_quat_inv(inv, d->xquat[1]);
     b_rotate(angl, d->cvel[1], inv);
   }
-  key_t2 rng = {{(uint32_t)st[PP3_S_RNG], (uint32_t)st[PP3_S_RNG + 1]}};
+  key_t2 rng = {{rngw[0], rngw[1]}};
   key_t2 nr = split_i(rng, 6, 0), ka = split_i(rng, 6, 1), kg = split_i(rng, 6, 2);
   key_t2 km = split_i(rng, 6, 3), kl = split_i(rng, 6, 4), ki = split_i(rng, 6, 5);
-  st[PP3_S_RNG] = (real)nr.k[0];
-  st[PP3_S_RNG + 1] = (real)nr.k[1];
+  rngw[0] = nr.k[0];
+  rngw[1] = nr.k[1];
   real imu[6];
   real g0[3] = {0, 0, -1}, g[3];
   b_rotate(g, g0, inv);
@@ -1360,15 +1360,16 @@ void orc_env_reset(const pp3_model_t* mm, const pp3_env_config_t* cfg, const dou
   forward(&e->m, d);
   for (int i = 0; i < NQ; i++) st[PP3_S_QPOS + i] = d->qpos[i];
   for (int i = 0; i < NV; i++) { st[PP3_S_QVEL + i] = d->qvel[i]; st[PP3_S_QACC_WS + i] = d->qacc_warmstart[i]; }
-  st[PP3_S_RNG] = (real)rng0.k[0];
-  st[PP3_S_RNG + 1] = (real)rng0.k[1];
+  uint32_t rngw[2] = {rng0.k[0], rng0.k[1]};
   real cmd[3], dz[3];
   sample_command(e, kcmd, cmd);
   sample_orientation(e, kori, dz);
   for (int k = 0; k < 3; k++) { st[PP3_S_COMMAND + k] = cmd[k]; st[PP3_S_DESIRED_Z + k] = dz[k]; }
   for (int l = 0; l < e->Li; l++) st[e->imu_off + 5 * e->Li + l] = -1; /* gravity z row */
-  get_obs(e, d, st, ob);
+  get_obs(e, d, st, rngw, ob);
   for (int k = 0; k < e->stride; k++) state[k] = (double)st[k];
+  state[PP3_S_RNG] = (double)rngw[0];
+  state[PP3_S_RNG + 1] = (double)rngw[1];
   for (int k = 0; k < PP3_OBS_DIM * e->H; k++) obs[k] = (double)ob[k];
   *reward = 0;
   *done = 0;
@@ -1381,18 +1382,18 @@ void orc_env_reset(const pp3_model_t* mm, const pp3_env_config_t* cfg, const dou
   free(st); free(ob); free(e); free(d);
 }
 
-static void env_step_impl(const Env* e, Data* d, real* st, real* ob, const double* action, double* reward, double* done,
-                          double* metrics, double* pipe) {
+static void env_step_impl(const Env* e, Data* d, real* st, uint32_t* rngw, real* ob, const double* action, double* reward,
+                          double* done, double* metrics, double* pipe) {
   const pp3_env_config_t* c = &e->c;
   const Model* m = &e->m;
   real dt = (real)c->dt;
   for (int i = 0; i < NQ; i++) d->qpos[i] = st[PP3_S_QPOS + i];
   for (int i = 0; i < NV; i++) { d->qvel[i] = st[PP3_S_QVEL + i]; d->qacc_warmstart[i] = st[PP3_S_QACC_WS + i]; }
-  key_t2 rng = {{(uint32_t)st[PP3_S_RNG], (uint32_t)st[PP3_S_RNG + 1]}};
+  key_t2 rng = {{rngw[0], rngw[1]}};
   key_t2 r0 = split_i(rng, 5, 0), kcmd = split_i(rng, 5, 1), kkick = split_i(rng, 5, 2);
   key_t2 kbern = split_i(rng, 5, 3), klat = split_i(rng, 5, 4);
-  st[PP3_S_RNG] = (real)r0.k[0];
-  st[PP3_S_RNG + 1] = (real)r0.k[1];
+  rngw[0] = r0.k[0];
+  rngw[1] = r0.k[1];
   /* kick (environment.py:352-356) */
   float bern = uniform_i(kbern, 1, 0, 0.0f, 1.0f) < (float)c->kick_probability ? 1.0f : 0.0f;
   float kick[2];
@@ -1419,7 +1420,7 @@ static void env_step_impl(const Env* e, Data* d, real* st, real* ob, const doubl
   for (int i = 0; i < NQ; i++) st[PP3_S_QPOS + i] = d->qpos[i];
   for (int i = 0; i < NV; i++) { st[PP3_S_QVEL + i] = d->qvel[i]; st[PP3_S_QACC_WS + i] = d->qacc_warmstart[i]; }
   /* observation (uses pre-update last_act / command) */
-  get_obs(e, d, st, ob);
+  get_obs(e, d, st, rngw, ob);
   /* brax x/xd of bodies (index b-1) */
   real xdv[NB][3], xda[NB][3];
   for (int b = 1; b < NB; b++) {
@@ -1572,8 +1573,11 @@ void orc_env_step(const pp3_model_t* mm, const pp3_env_config_t* cfg, const doub
   real* ob = (real*)malloc(sizeof(real) * PP3_OBS_DIM * e->H);
   for (int k = 0; k < e->stride; k++) st[k] = (real)state[k];
   for (int k = 0; k < PP3_OBS_DIM * e->H; k++) ob[k] = (real)obs[k];
-  env_step_impl(e, d, st, ob, action, reward, done, metrics, pipe);
+  uint32_t rngw[2] = {(uint32_t)state[PP3_S_RNG], (uint32_t)state[PP3_S_RNG + 1]};
+  env_step_impl(e, d, st, rngw, ob, action, reward, done, metrics, pipe);
   for (int k = 0; k < e->stride; k++) state[k] = (double)st[k];
+  state[PP3_S_RNG] = (double)rngw[0];
+  state[PP3_S_RNG + 1] = (double)rngw[1];
   for (int k = 0; k < PP3_OBS_DIM * e->H; k++) obs[k] = (double)ob[k];
   free(st); free(ob); free(e); free(d);
 }
@@ -1600,14 +1604,17 @@ int orc_env_rollout(const pp3_model_t* mm, const pp3_env_config_t* cfg, int n, i
     real* ob = (real*)malloc(sizeof(real) * PP3_OBS_DIM * e->H);
     for (int k = 0; k < e->stride; k++) st[k] = (real)states[(size_t)i * e->stride + k];
     for (int k = 0; k < PP3_OBS_DIM * e->H; k++) ob[k] = (real)obs[(size_t)i * PP3_OBS_DIM * e->H + k];
+    uint32_t rngw[2] = {(uint32_t)states[(size_t)i * e->stride + PP3_S_RNG], (uint32_t)states[(size_t)i * e->stride + PP3_S_RNG + 1]};
     double zero[12] = {0};
     for (int s = 0; s < nsteps; s++) {
       double rew, dn, met[PP3_NMETRIC];
       const double* a = actions ? actions + ((size_t)s * n + i) * 12 : zero;
-      env_step_impl(e, d, st, ob, a, &rew, &dn, met, NULL);
+      env_step_impl(e, d, st, rngw, ob, a, &rew, &dn, met, NULL);
       if (rewards) rewards[(size_t)s * n + i] = rew;
     }
     for (int k = 0; k < e->stride; k++) states[(size_t)i * e->stride + k] = (double)st[k];
+    states[(size_t)i * e->stride + PP3_S_RNG] = (double)rngw[0];
+    states[(size_t)i * e->stride + PP3_S_RNG + 1] = (double)rngw[1];
     for (int k = 0; k < PP3_OBS_DIM * e->H; k++) obs[(size_t)i * PP3_OBS_DIM * e->H + k] = (double)ob[k];
     free(st); free(ob); free(d);
   }

@@ -1,0 +1,54 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/pupper_hip.h declares."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from pupperv3_mjx import _abi, _lib
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "pupper_hip.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(pp3_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_what_python_binds():
+    assert set(_declared()) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_loads_and_exports_all_symbols():
+    L = _lib.load()
+    for name in _declared():
+        assert hasattr(L, name), name
+    assert L.pp3_abi_version() == _abi.ABI_VERSION
+
+
+def test_struct_layouts_match_ctypes():
+    L = _lib.load()
+    assert L.pp3_struct_size(0) == C.sizeof(_abi.Model)
+    assert L.pp3_struct_size(1) == C.sizeof(_abi.EnvConfig)
+    assert 0 < L.pp3_struct_size(3) <= 20 * 1024  # LDS per env (one workgroup)
+
+
+def test_create_rejects_bad_config_without_gpu_work():
+    """pp3_create validates model/config before touching the device."""
+    import common
+    m, c, _ = common.env_model_and_config(common.MODEL_XML)
+    L = _lib.load()
+    h = C.c_void_p()
+    c.obs_history = 99
+    rc = L.pp3_create(C.byref(m), C.byref(c), 4, 0, C.byref(h))
+    assert rc == 1 and b"observation_history" in L.pp3_last_error()
+    c.obs_history = 2
+    m2 = _abi.Model.from_buffer_copy(m)
+    m2.cone = 1
+    rc = L.pp3_create(C.byref(m2), C.byref(c), 4, 0, C.byref(h))
+    assert rc == 2
+
+
+def test_state_layout_constants():
+    assert _abi.state_stride(2, 2) == 98 + 24 + 12
+    assert _abi.REWARD_NAMES[_abi.NREWARD - 1] == "body_collision"

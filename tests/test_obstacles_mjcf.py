@@ -1,0 +1,94 @@
+"""obstacles.py golden fixture (generated from the reference module), MJCF compiler, XML editors."""
+import json
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+
+import common
+from pupperv3_mjx import MODEL_XML, _abi, mjcf, obstacles, utils
+
+
+@pytest.mark.parametrize("case", ["seed0_n10_len6.0", "seed3_n25_len3.0"])
+def test_obstacles_match_reference_golden(case):
+    gold = json.load(open(os.path.join(common.GOLDEN, "obstacles_golden.json")))[case]
+    seed = int(case.split("_")[0][4:])
+    n = int(case.split("_")[1][1:])
+    length = float(case.split("len")[1])
+    tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
+    obstacles.add_boxes_to_model(tree, n_boxes=n, x_range=(-5, 5), y_range=(-5, 5), height=0.02, length=length,
+                                 seed=seed)
+    boxes = [dict(g.attrib) for g in tree.getroot().find("worldbody").findall("geom")
+             if g.get("name", "").startswith("box_geom_")]
+    assert boxes == gold
+
+
+def test_model_counts():
+    cm = mjcf.load(MODEL_XML)
+    m = cm.struct
+    assert cm.ngeom == 23 and m.ncgeom == 9 and m.npair == 32 and m.nsite == 5
+    assert abs(sum(m.body_mass[:]) - 3.17) < 1e-12
+    assert list(cm.body_geom_ids("base_link")) == [2]
+    assert [list(cm.body_geom_ids(n)) for n in ("leg_front_r_2", "leg_front_l_2", "leg_back_r_2", "leg_back_l_2")] \
+        == [[4, 5], [9, 10], [14, 15], [19, 20]]
+    assert cm.site_id("leg_back_l_3_foot_site") == 4
+    assert list(m.dof_armature[:6]) == [0] * 6 and list(m.dof_armature[6:]) == [0.0016] * 12
+    assert list(m.dof_frictionloss[6:]) == [0.125] * 12 and list(m.dof_damping[6:]) == [0.01] * 12
+    assert list(m.jnt_limited[:]) == [0] + [1] * 12
+    assert list(m.actuator_forcelimited[:]) == [1] * 12 and list(m.actuator_ctrllimited[:]) == [0] * 12
+    assert m.iterations == 1 and m.ls_iterations == 5 and m.impratio == 10 and m.eulerdamp == 0
+    assert m.max_contact_points == 5 and m.max_geom_pairs == 4
+    # the 8 sphere-plane + 24 sphere-sphere candidates (parent-child legs filtered)
+    types = [(m.cgeom_type[m.pair_g1[p]], m.cgeom_type[m.pair_g2[p]]) for p in range(m.npair)]
+    assert types.count((0, 2)) == 8 and types.count((2, 2)) == 24
+
+
+def test_obstacle_model_pairs():
+    xml = common.model_with_obstacles_xml(10)
+    cm = mjcf.load(xml, is_string=True)
+    assert cm.ngeom == 33 and cm.struct.npair == 32 + 80
+
+
+def test_invweight_and_mass_matrix_cross_check():
+    """mjcf's numpy M (sum of J'MJ) equals the oracle's CRB M; invweight0 is diag-based and positive."""
+    from oracle import oracle as O
+    cm = common.pd_model()
+    m = cm.struct
+    rs = np.random.RandomState(0)
+    for _ in range(5):
+        q = np.zeros(19)
+        q[:3] = rs.normal(size=3)
+        qq = rs.normal(size=4)
+        q[3:7] = qq / np.linalg.norm(qq)
+        q[7:] = rs.uniform(-1, 1, 12)
+        M_np, _, _, _ = mjcf.mass_matrix_and_jacobians(m, q)
+        M_or = O.mj_forward(m, q, np.zeros(18), np.zeros(18), np.zeros(12))["M"]
+        np.testing.assert_allclose(M_or, M_np, rtol=1e-10, atol=1e-12)
+        assert np.all(np.linalg.eigvalsh(M_or) > 0)
+    assert np.all(np.array(m.dof_invweight0[:]) > 0)
+    assert np.all(np.array(m.body_invweight0[1:]) > 0)
+    assert abs(m.meaninertia - np.trace(mjcf.mass_matrix_and_jacobians(m, np.array(m.qpos0[:]))[0]) / 18) < 1e-12
+
+
+def test_set_starting_position():
+    tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
+    utils.set_robot_starting_position(tree, starting_pos=[0.1, 0.2, 0.5], starting_quat=[0.1, 0.2, 0.3, 0.4])
+    body = tree.find(".//worldbody/body[@name='base_link']")
+    assert body.get("pos").split(" ") == ["0.1", "0.2", "0.5"]
+    assert body.get("quat").split(" ") == ["0.1", "0.2", "0.3", "0.4"]
+    home = tree.find(".//keyframe/key[@name='home']")
+    assert list(map(float, home.get("qpos").split(" ")))[:7] == [0.1, 0.2, 0.5, 0.1, 0.2, 0.3, 0.4]
+
+
+def test_set_mjx_custom_options():
+    tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
+    utils.set_mjx_custom_options(tree, max_contact_points=9, max_geom_pairs=7)
+    cm = mjcf.load(tree)
+    assert cm.struct.max_contact_points == 9 and cm.struct.max_geom_pairs == 7
+
+
+def test_unsupported_features_fail_loudly():
+    xml = open(MODEL_XML).read().replace('cone="pyramidal"', 'cone="elliptic"')
+    with pytest.raises(NotImplementedError):
+        mjcf.load(xml, is_string=True)
