@@ -336,7 +336,11 @@ int pp3_memcpy_d2d(void* dst_dev, const void* src_dev, size_t bytes, void* strea
  * keyed by (seed, step) on device; record HIP events around the step kernel
  * launches on the handle's stream so the average kernel duration can be read. */
 int pp3_fill_uniform(pp3_env_t* env, float* dev, int64_t count, uint32_t seed, uint32_t ctr, float lo, float hi, void* stream);
-int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int32_t nsteps, float* kernel_ms_total);
+/* nsteps back-to-back pp3_step launches on the handle's stream, step i reading actions
+ * actions_dev + i * action_stride (elements; 0 = reuse); HIP events bracket the launches and
+ * kernel_ms_total receives their elapsed time. */
+int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stride, int32_t nsteps,
+                   float* kernel_ms_total);
 
 #ifdef __cplusplus
 }

@@ -1914,12 +1914,13 @@ int pp3_fill_uniform(pp3_env_t* e, float* dev, int64_t count, uint32_t seed, uin
   return PP3_OK;
 }
 
-int pp3_step_timed(pp3_env_t* e, const float* actions_dev, int32_t nsteps, float* kernel_ms_total) {
+int pp3_step_timed(pp3_env_t* e, const float* actions_dev, int64_t action_stride, int32_t nsteps,
+                   float* kernel_ms_total) {
   if (!e || !actions_dev || !kernel_ms_total) return set_err(PP3_ERR_ARG, "null argument");
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipEventRecord(e->ev0, e->stream));
   for (int i = 0; i < nsteps; i++) {
-    int rc = pp3_step(e, actions_dev, e->stream);
+    int rc = pp3_step(e, actions_dev + (size_t)i * (size_t)action_stride, e->stream);
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(e->ev1, e->stream));

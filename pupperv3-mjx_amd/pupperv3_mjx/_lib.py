@@ -55,7 +55,7 @@ def load() -> C.CDLL:
     L.pp3_memcpy_d2h.argtypes = [vp, vp, sz]
     L.pp3_memcpy_d2d.argtypes = [vp, vp, sz, vp]
     L.pp3_fill_uniform.argtypes = [vp, vp, i64, C.c_uint32, C.c_uint32, C.c_float, C.c_float, vp]
-    L.pp3_step_timed.argtypes = [vp, vp, i32, C.POINTER(C.c_float)]
+    L.pp3_step_timed.argtypes = [vp, vp, i64, i32, C.POINTER(C.c_float)]
     for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
                  "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",

@@ -82,8 +82,8 @@ def main():
         buf.upload(act)
         import ctypes as C
         ms = C.c_float()
-        _lib.check(envb._L.pp3_step_timed(envb._h, buf.ptr, 5, C.byref(ms)))
-        _lib.check(envb._L.pp3_step_timed(envb._h, buf.ptr, 20, C.byref(ms)))
+        _lib.check(envb._L.pp3_step_timed(envb._h, buf.ptr, 0, 5, C.byref(ms)))
+        _lib.check(envb._L.pp3_step_timed(envb._h, buf.ptr, 0, 20, C.byref(ms)))
         print(f"N={N}: {ms.value / 20:.3f} ms/step -> {N * 20 / (ms.value / 1e3) / 1e6:.2f} M env-steps/s")
 
 
