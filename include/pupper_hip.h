@@ -188,7 +188,7 @@ typedef struct pp3_env_config_t {
   int32_t n_torso_geoms;
   int32_t torso_geoms[8];
   int32_t rng_partitionable;   /* jax_threefry_partitionable (jax 0.5.0: 1) */
-  int32_t pad0;
+  int32_t ncon_max;            /* contact cap per env: 0 = auto (8 flat, 16 with boxes), 8, 16 */
   double latency_dist[PP3_MAX_LAG];
   double imu_latency_dist[PP3_MAX_LAG];
   double action_scale;
@@ -341,6 +341,10 @@ int pp3_fill_uniform(pp3_env_t* env, float* dev, int64_t count, uint32_t seed, u
  * kernel_ms_total receives their elapsed time. */
 int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stride, int32_t nsteps,
                    float* kernel_ms_total);
+
+/* Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-clock totals of env_step_kernel
+ * summed over envs (n <= 16 slots); returns PP3_ERR_ARG in the production build. */
+int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset);
 
 #ifdef __cplusplus
 }

@@ -95,7 +95,7 @@ void orc_threefry2x32(uint32_t k0, uint32_t k1, uint32_t x0, uint32_t x1, uint32
 typedef struct { uint32_t k[2]; } key_t2;
 
 static int g_partitionable = 1;
-static int g_ncon_max = 16; /* contact cap shared with the HIP kernel (PP3 kernel NCON_MAX) */
+static int g_ncon_max = 0; /* contact cap shared with the HIP kernel: 0 = auto (8 flat, 16 with boxes) */
 
 /* jax.random.split(key, n)[i] */
 static key_t2 split_i(key_t2 key, int n, int i) {
@@ -400,7 +400,12 @@ static void model_from_abi(Model* M, const pp3_model_t* m, const real* dr) {
       M->act_ctrlrange[a][k] = (real)m->actuator_ctrlrange[a][k];
     }
   }
-  M->ncon_max = g_ncon_max;
+  {
+    int has_static_solid = 0;
+    for (int g = 0; g < m->ncgeom; g++)
+      if (m->cgeom_bodyid[g] == 0 && m->cgeom_type[g] != PP3_GEOM_PLANE) has_static_solid = 1;
+    M->ncon_max = g_ncon_max > 0 ? g_ncon_max : (has_static_solid ? 16 : 8);
+  }
   if (dr) {
     /* domain_randomization.py:21-66: one friction scalar for all geoms, Kp/Kd for all
      * actuators, torso COM shift, elementwise inertia / mass scales (values absolute). */
@@ -1335,6 +1340,7 @@ static void env_setup(Env* e, const pp3_model_t* mm, const pp3_env_config_t* cfg
   e->imu_off = PP3_S_ACT_BUF + 12 * e->La;
   e->stride = e->imu_off + 6 * e->Li;
   e->m.timestep = (real)mm->timestep;
+  if (cfg->ncon_max > 0) e->m.ncon_max = cfg->ncon_max;
   g_partitionable = cfg->rng_partitionable;
 }
 

@@ -14,11 +14,9 @@ constexpr int NV = PP3_NV;
 constexpr int NQ = PP3_NQ;
 constexpr int NU = PP3_NU;
 constexpr int WAVE = 64;
-constexpr int NCMAX = 16;                 // contact cap per env (deepest kept), == oracle ncon_max
 constexpr int NLMAX = 24;                 // joint-limit rows (12 joints x 2 sides)
 constexpr int NFR = 12;                   // frictionloss rows (hinge dofs)
-constexpr int NEFC_MAX = NFR + NLMAX + 4 * NCMAX;
-constexpr int MAX_ROBOT_GEOM = 16;        // collidable geoms on moving bodies
+constexpr int MAX_ROBOT_GEOM = 16;        // DevModel table size for collidable geoms on moving bodies
 constexpr int NMPAIR_MAX = 128;           // nonzero (i, j<=i) entries of M
 constexpr float MINVAL = 1e-15f;
 constexpr float MINIMP = 0.0001f;
@@ -261,7 +259,7 @@ __device__ __forceinline__ uint32_t bits_i(Key k, int count, int i, int part) {
   return half ? y1 : y0;
 }
 // jax.random.uniform element i of `count`, float32, no FMA contraction (bit-exact with JAX)
-__device__ __attribute__((noinline)) float uniform_i(Key k, int count, int i, float lo, float hi, int part) {
+__device__ __forceinline__ float uniform_i(Key k, int count, int i, float lo, float hi, int part) {
 #pragma clang fp contract(off)
   uint32_t b = (bits_i(k, count, i, part) >> 9) | 0x3F800000u;
   float u = __uint_as_float(b) - 1.0f;

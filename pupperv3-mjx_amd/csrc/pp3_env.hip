@@ -5,9 +5,10 @@
 // latency prologue, n_frames (=5) MuJoCo-semantics physics substeps (kinematics, CRB mass
 // matrix, collision, pyramidal contact + frictionloss + limit constraints, RNE, Newton
 // solve with exact line search, Euler), then the observation/reward/termination epilogue.
-// Per-env state lives in LDS for the whole launch; HBM sees one read and one write of the
-// env's state record per env step.  Small dense linear algebra (18x18 LDL^T) runs in
-// registers, one matrix row per lane, with v_readlane broadcasts.
+// Per-env state lives in LDS for the whole launch (<= 10 KB per env so 16 envs = 16 waves
+// are resident per CU); HBM sees one read and one write of the env's state record per env
+// step.  Small dense linear algebra (18x18 LDL^T) runs in registers, one matrix row per
+// lane, with v_readlane broadcasts.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -15,142 +16,176 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <mutex>
 #include <string>
-#include <vector>
 
 #include "pp3_device.h"
 
 namespace pp3 {
 
-constexpr int STRIDE_MAX = PP3_S_ACT_BUF + 12 * PP3_MAX_LAG + 6 * PP3_MAX_LAG;
 constexpr int HMAX = 16;  // observation_history limit
 constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + WAVE - 1) / WAVE;
+constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
 
+// Phase-local scratch that never lives across a phase boundary it does not own.
+template <int NC>
+union Scratch {
+  float xipos[NB][3];      // phase 1 (kinematics) -> phase 2 (com_pos)
+  struct {                 // phases 3-4
+    float F[NV][6];        // crb*cdof -> M entries
+    float cacc[NB][6];     // rne chain -> body forces (overwritten in place by cfrc)
+    float hit_dist[WAVE];  // collision overflow ranking
+    int hit_pair[WAVE];
+    float con_pos[NC][3];  // collision -> contact Jacobians
+    float con_frame[NC][9];
+  } a;
+  float L[NV][NV + 1];     // LDL factor rows (transposed reads), phases 6-8
+  struct {                 // env prologue / epilogue
+    float u[40];
+    float o[PP3_OBS_DIM];
+    float rw[PP3_NREWARD];
+    float xdv[NB][3], xda[NB][3];
+    int contact[4], filt_mm[4], filt_cm[4];
+    float first[4];
+    int done;
+    float knee, bodyc;
+  } e;
+};
+
+template <int NC>
 struct alignas(16) Shared {
+  static constexpr int NEFC = NFR + NLMAX + 4 * NC;
   float qpos[20], qvel[20], qws[20], qacc[20], ctrl[12];
-  float xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3];
-  float xanchor[NJ][3], xaxis[NJ][3];
-  float com[4];
-  float cinert[NB][10];
-  float cdof[NV][6];
-  float F[NV][6];
-  float cvel[NB][6];
-  float cfrc[NB][6];  // subtree-accumulated (legs) / own (base) RNE body forces
-  float M[NV][NV + 1];
-  float L[NV][NV + 1];
-  float gxpos[MAX_ROBOT_GEOM][3];
-  float site_xpos[PP3_MAX_SITE][3];
+  float st[PP3_S_ACT_BUF];  // head of the state record (latency buffers stay in HBM)
   // per-env dynamic parameters (domain randomisation)
   float mass[NB], inertia[NB][3], ipos[NB][3];
   float fric, kp, kd;
   int dr_on;
-  // forces / accelerations
-  float qfrc_bias[NV], qfrc_smooth[NV], qfrc_act[NV], qacc_smooth[NV], Ma[NV], grad[NV], search[NV], dofD[NV];
+  // kinematics / dynamics of the current substep (the last one feeds the epilogue)
+  float xpos[NB][3], xquat[NB][4], xaxis[NJ][3];
+  float com[4];
+  float cinert[NB][10];
+  float cdof[NV][6];
+  float cvel[NB][6];
+  float M[NV][NV + 1];
+  float gxpos[NROBOT_GEOM][3];
+  float foot_xpos[4][3];
+  float qfrc_smooth[NV], qfrc_act[NV], qacc_smooth[NV], Ma[NV], grad[NV], search[NV], dofD[NV];
   // contacts
-  int ncon, nhit;
-  int con_pair[NCMAX];
-  float con_pos[NCMAX][3], con_frame[NCMAX][9], con_dist[NCMAX], con_mu[NCMAX];
-  float con_G[NCMAX][5];
-  float Jc[NCMAX][3][NV + 2];
-  float hit_dist[WAVE];
-  int hit_pair[WAVE];
+  int ncon, nhit, nl;
+  int con_pair[NC];
+  float con_dist[NC], con_mu[NC];
+  float con_G[NC][5];
+  float Jc[NC][3][NV];
   // constraint rows
-  int nl;
   int lim_dof[NLMAX];
   float lim_sgn[NLMAX];
-  float efc_D[NEFC_MAX], efc_R[NEFC_MAX], efc_aref[NEFC_MAX], efc_force[NEFC_MAX];
-  // env scratch
-  float st[STRIDE_MAX];
-  uint32_t keys[8][2];
-  float u[40];
-  float o[PP3_OBS_DIM];
-  float rw[PP3_NREWARD];
-  float xdv[NB][3], xda[NB][3];
-  int contact[4], filt_mm[4], filt_cm[4];
-  float first[4];
-  int done;
-  float knee, bodyc;
-  int li;
+  float efc_D[NEFC], efc_R[NEFC], efc_aref[NEFC], efc_force[NEFC];
+  Scratch<NC> x;
+#ifdef PP3_PHASE_PROF
+  uint64_t prof[16];
+  uint64_t prof_t;
+#endif
 };
 
 #define SYNC() __syncthreads()
 
-__device__ __forceinline__ Key key_of(const Shared& s, int i) { return Key{s.keys[i][0], s.keys[i][1]}; }
+// Diagnostic build only (-DPP3_PHASE_PROF): per-phase s_memtime deltas summed over all envs.
+#ifdef PP3_PHASE_PROF
+constexpr int NPROF = 16;
+__device__ unsigned long long g_prof[NPROF];
+#define PHASE(k)                                                          \
+  do {                                                                    \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                     \
+    if (lane == 0) { s.prof[k] += t_ - s.prof_t; s.prof_t = t_; }         \
+  } while (0)
+#else
+#define PHASE(k) do { } while (0)
+#endif
+
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // ------------------------------------------------------------------------------------
-// Phase 1: forward kinematics (mj_kinematics).  Lanes 0..3 each walk base -> leg chain.
+// Phase 1: forward kinematics (mj_kinematics).  12 lanes build the local link rotations
+// (body_quat * joint rotation) in parallel, then lanes 0..3 compose base -> leg chain.
+// Hinge anchors coincide with body origins (jnt_pos = 0, checked at pp3_create).
 // ------------------------------------------------------------------------------------
-__device__ void kinematics(Shared& s, const DevModel& m, int lane) {
+template <int NC>
+__device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int lane) {
+  // local quaternion of link (leg l, level k) in lane 4k + l (lanes 0..11)
+  float lq[4] = {1, 0, 0, 0};
+  if (lane < 12) {
+    const int l = lane & 3, k = lane >> 2;
+    const int b = 2 + 3 * l + k, j = 1 + 3 * l + k, qa = 7 + 3 * l + k;
+    float qloc[4];
+    axisangle2quat(qloc, m.jnt_axis[j], s.qpos[qa] - m.qpos0[qa]);
+    mulquat(lq, m.body_quat[b], qloc);
+  }
+  // broadcast the 3 levels of this lane's leg (lanes 0..3 consume)
+  float lq1[4], lq2[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    lq1[c] = __shfl(lq[c], (lane & 3) + 4, WAVE);
+    lq2[c] = __shfl(lq[c], (lane & 3) + 8, WAVE);
+  }
   if (lane < 4) {
-    float bq[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
-    normalize4(bq);
+    float pq[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
+    normalize4(pq);
     float pp[3] = {s.qpos[0], s.qpos[1], s.qpos[2]};
-    float pq[4] = {bq[0], bq[1], bq[2], bq[3]};
     float pR[9];
     quat2mat(pq, pR);
     if (lane == 0) {
       float off[3];
       matvec(off, pR, s.ipos[1]);
-      for (int k = 0; k < 3; k++) {
-        s.xpos[1][k] = pp[k];
-        s.xipos[1][k] = pp[k] + off[k];
-        s.xanchor[0][k] = pp[k];
-        s.xaxis[0][k] = m.jnt_axis[0][k];
+      for (int c = 0; c < 3; c++) {
+        s.xpos[1][c] = pp[c];
+        s.x.xipos[1][c] = pp[c] + off[c];
+        s.xaxis[0][c] = m.jnt_axis[0][c];
       }
-      for (int k = 0; k < 4; k++) s.xquat[1][k] = pq[k];
-      for (int k = 0; k < 9; k++) s.xmat[1][k] = pR[k];
+      for (int c = 0; c < 4; c++) s.xquat[1][c] = pq[c];
     }
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      const int b = 2 + 3 * lane + k, j = 1 + 3 * lane + k, qa = 7 + 3 * lane + k;
-      float xp[3], xq[4], off[3], R[9], ax[3], an[3], qloc[4], v[3];
+      const int b = 2 + 3 * lane + k, j = 1 + 3 * lane + k;
+      const float* lqk = k == 0 ? lq : (k == 1 ? lq1 : lq2);
+      float xp[3], xq[4], off[3], R[9], ax[3];
       matvec(off, pR, m.body_pos[b]);
       for (int c = 0; c < 3; c++) xp[c] = pp[c] + off[c];
-      mulquat(xq, pq, m.body_quat[b]);
-      quat2mat(xq, R);
-      matvec(ax, R, m.jnt_axis[j]);
-      matvec(an, R, m.jnt_pos[j]);
-      for (int c = 0; c < 3; c++) an[c] += xp[c];
-      axisangle2quat(qloc, m.jnt_axis[j], s.qpos[qa] - m.qpos0[qa]);
-      mulquat(xq, xq, qloc);
-      quat2mat(xq, R);
-      matvec(v, R, m.jnt_pos[j]);
-      for (int c = 0; c < 3; c++) xp[c] = an[c] - v[c];
+      mulquat(xq, pq, lqk);
       normalize4(xq);
       quat2mat(xq, R);
+      matvec(ax, R, m.jnt_axis[j]);
       matvec(off, R, s.ipos[b]);
       for (int c = 0; c < 3; c++) {
         s.xpos[b][c] = xp[c];
-        s.xipos[b][c] = xp[c] + off[c];
+        s.x.xipos[b][c] = xp[c] + off[c];
         s.xaxis[j][c] = ax[c];
-        s.xanchor[j][c] = an[c];
         pp[c] = xp[c];
       }
       for (int c = 0; c < 4; c++) { s.xquat[b][c] = xq[c]; pq[c] = xq[c]; }
-      for (int c = 0; c < 9; c++) { s.xmat[b][c] = R[c]; pR[c] = R[c]; }
+      for (int c = 0; c < 9; c++) pR[c] = R[c];
     }
   }
 }
 
 // ------------------------------------------------------------------------------------
-// Phase 2: subtree com, cinert (mju_inertCom), cdof, robot geom and site positions.
+// Phase 2: subtree com, cinert (mju_inertCom), cdof, robot geom and foot-site positions.
 // ------------------------------------------------------------------------------------
-__device__ void com_pos(Shared& s, const DevModel& m, int lane) {
+template <int NC>
+__device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int lane) {
   float mb = 0, mx = 0, my = 0, mz = 0;
   if (lane >= 1 && lane < NB) {
     mb = s.mass[lane];
-    mx = mb * s.xipos[lane][0];
-    my = mb * s.xipos[lane][1];
-    mz = mb * s.xipos[lane][2];
+    mx = mb * s.x.xipos[lane][0];
+    my = mb * s.x.xipos[lane][1];
+    mz = mb * s.x.xipos[lane][2];
   }
   mb = wave_sum(mb);
   mx = wave_sum(mx);
   my = wave_sum(my);
   mz = wave_sum(mz);
   float com[3];
-  if (mb > MINVAL) { com[0] = mx / mb; com[1] = my / mb; com[2] = mz / mb; }
-  else { com[0] = s.xipos[1][0]; com[1] = s.xipos[1][1]; com[2] = s.xipos[1][2]; }
+  if (mb > MINVAL) { const float im = 1.0f / mb; com[0] = mx * im; com[1] = my * im; com[2] = mz * im; }
+  else { com[0] = s.x.xipos[1][0]; com[1] = s.x.xipos[1][1]; com[2] = s.x.xipos[1][2]; }
   if (lane == 0) { s.com[0] = com[0]; s.com[1] = com[1]; s.com[2] = com[2]; }
   if (lane >= 1 && lane < NB) {
     const int b = lane;
@@ -164,8 +199,8 @@ __device__ void com_pos(Shared& s, const DevModel& m, int lane) {
 #pragma unroll
       for (int j = 0; j < 3; j++)
         A[i][j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
-    float mm = s.mass[b];
-    float dx = s.xipos[b][0] - com[0], dy = s.xipos[b][1] - com[1], dz = s.xipos[b][2] - com[2];
+    const float mm = s.mass[b];
+    const float dx = s.x.xipos[b][0] - com[0], dy = s.x.xipos[b][1] - com[1], dz = s.x.xipos[b][2] - com[2];
     float* r = s.cinert[b];
     r[0] = A[0][0] + mm * (dy * dy + dz * dz);
     r[1] = A[1][1] + mm * (dx * dx + dz * dz);
@@ -183,40 +218,33 @@ __device__ void com_pos(Shared& s, const DevModel& m, int lane) {
       cd[3 + d] = 1;
     } else {
       float ax[3], off[3], c[3];
-      int j;
+      int b;
       if (d < 6) {
-        ax[0] = s.xmat[1][d - 3]; ax[1] = s.xmat[1][3 + d - 3]; ax[2] = s.xmat[1][6 + d - 3];
-        j = 0;
+        float R[9];
+        quat2mat(s.xquat[1], R);
+        ax[0] = R[d - 3]; ax[1] = R[3 + d - 3]; ax[2] = R[6 + d - 3];
+        b = 1;
       } else {
-        j = d - 5;
+        const int j = d - 5;
         ax[0] = s.xaxis[j][0]; ax[1] = s.xaxis[j][1]; ax[2] = s.xaxis[j][2];
+        b = 2 + (d - 6);
       }
-      for (int k = 0; k < 3; k++) off[k] = com[k] - s.xanchor[j][k];
+      for (int k = 0; k < 3; k++) off[k] = com[k] - s.xpos[b][k];
       cross3(c, ax, off);
       for (int k = 0; k < 3; k++) { cd[k] = ax[k]; cd[3 + k] = c[k]; }
     }
   } else if (lane >= 32 && lane < 32 + m.nrobot_geom) {
     const int g = m.robot_geom[lane - 32], b = m.cg_body[g];
-    float off[3];
-    matvec(off, s.xmat[b], m.cg_pos[g]);
+    float R[9], off[3];
+    quat2mat(s.xquat[b], R);
+    matvec(off, R, m.cg_pos[g]);
     for (int k = 0; k < 3; k++) s.gxpos[lane - 32][k] = s.xpos[b][k] + off[k];
-  } else if (lane >= 48 && lane < 48 + m.nsite) {
-    const int si = lane - 48, b = m.site_body[si];
-    float off[3];
-    matvec(off, s.xmat[b], m.site_pos[si]);
-    for (int k = 0; k < 3; k++) s.site_xpos[si][k] = s.xpos[b][k] + off[k];
-  }
-}
-
-// geometry of collidable geom g in this env
-__device__ __forceinline__ void geom_pose(const Shared& s, const DevModel& m, int g, float p[3], const float** R) {
-  const int slot = m.cg_slot[g];
-  if (slot >= 0) {
-    p[0] = s.gxpos[slot][0]; p[1] = s.gxpos[slot][1]; p[2] = s.gxpos[slot][2];
-    *R = s.xmat[m.cg_body[g]];  // sphere orientation is irrelevant; body frame is fine
-  } else {
-    p[0] = m.cg_pos[g][0]; p[1] = m.cg_pos[g][1]; p[2] = m.cg_pos[g][2];
-    *R = m.cg_wmat[g];
+  } else if (lane >= 48 && lane < 52) {
+    const int f = lane - 48, si = m.feet_site[f], b = m.site_body[si];
+    float R[9], off[3];
+    quat2mat(s.xquat[b], R);
+    matvec(off, R, m.site_pos[si]);
+    for (int k = 0; k < 3; k++) s.foot_xpos[f][k] = s.xpos[b][k] + off[k];
   }
 }
 
@@ -236,15 +264,20 @@ __device__ __forceinline__ void make_frame(float f[9], const float nin[3]) {
 }
 
 // narrow phase for pair p; returns hit and fills dist/pos/normal
-__device__ bool narrow(const Shared& s, const DevModel& m, int p, float& dist, float pos[3], float nrm[3]) {
+template <int NC>
+__device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, int p, float& dist, float pos[3],
+                                       float nrm[3]) {
   const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
   const int t1 = m.cg_type[g1], t2 = m.cg_type[g2];
   const float margin = m.pair_margin[p];
   float p1[3], p2[3];
-  const float *R1, *R2;
-  geom_pose(s, m, g1, p1, &R1);
-  geom_pose(s, m, g2, p2, &R2);
+  const int s1 = m.cg_slot[g1], s2 = m.cg_slot[g2];
+  for (int k = 0; k < 3; k++) {
+    p1[k] = s1 >= 0 ? s.gxpos[s1][k] : m.cg_pos[g1][k];
+    p2[k] = s2 >= 0 ? s.gxpos[s2][k] : m.cg_pos[g2][k];
+  }
   if (t1 == PP3_GEOM_PLANE && t2 == PP3_GEOM_SPHERE) {
+    const float* R1 = m.cg_wmat[g1];
     float nz[3] = {R1[2], R1[5], R1[8]};
     float v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
     float r = m.cg_size[g2][0];
@@ -265,6 +298,7 @@ __device__ bool narrow(const Shared& s, const DevModel& m, int p, float& dist, f
     return true;
   }
   if (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_BOX) {
+    const float* R2 = m.cg_wmat[g2];
     const float* h = m.cg_size[g2];
     float r = m.cg_size[g1][0];
     float rel[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]}, dl[3], cl[3];
@@ -284,14 +318,13 @@ __device__ bool narrow(const Shared& s, const DevModel& m, int p, float& dist, f
       if (len < MINVAL) { nl[0] = 0; nl[1] = 0; nl[2] = -1; }
       else { for (int k = 0; k < 3; k++) nl[k] = v[k] / len; }
     } else {
-      int ax = 0;
-      float best = h[0] - fabsf(dl[0]);
-      for (int k = 1; k < 3; k++) {
-        float t = h[k] - fabsf(dl[k]);
-        if (t < best) { best = t; ax = k; }
-      }
-      nl[0] = nl[1] = nl[2] = 0;
-      nl[ax] = dl[ax] >= 0 ? -1.0f : 1.0f;
+      const float t0 = h[0] - fabsf(dl[0]), t1b = h[1] - fabsf(dl[1]), t2b = h[2] - fabsf(dl[2]);
+      const int ax = (t1b < t0 && t1b <= t2b) ? 1 : (t2b < t0 && t2b < t1b) ? 2 : 0;
+      const float best = ax == 0 ? t0 : (ax == 1 ? t1b : t2b);
+      const float sg = (ax == 0 ? dl[0] : (ax == 1 ? dl[1] : dl[2])) >= 0 ? -1.0f : 1.0f;
+      nl[0] = ax == 0 ? sg : 0.0f;
+      nl[1] = ax == 1 ? sg : 0.0f;
+      nl[2] = ax == 2 ? sg : 0.0f;
       dd = -best - r;
     }
     matvec(nrm, R2, nl);
@@ -302,46 +335,47 @@ __device__ bool narrow(const Shared& s, const DevModel& m, int p, float& dist, f
   return false;
 }
 
-__device__ __forceinline__ void store_contact(Shared& s, const DevModel& m, int slot, int p, float dist,
+template <int NC>
+__device__ __forceinline__ void store_contact(Shared<NC>& s, const DevModel& m, int slot, int p, float dist,
                                               const float pos[3], const float nrm[3]) {
   s.con_pair[slot] = p;
   s.con_dist[slot] = dist;
-  for (int k = 0; k < 3; k++) s.con_pos[slot][k] = pos[k];
-  make_frame(s.con_frame[slot], nrm);
+  for (int k = 0; k < 3; k++) s.x.a.con_pos[slot][k] = pos[k];
+  make_frame(s.x.a.con_frame[slot], nrm);
   s.con_mu[slot] = s.dr_on ? s.fric : m.pair_mu[p];
 }
 
 // Phase 3a: collision (mj_collision), contacts compacted in pair order; when more than
-// NCMAX pairs penetrate, the NCMAX deepest are kept (same rule as the oracle).
-__device__ void collision(Shared& s, const DevModel& m, int lane) {
+// NC pairs penetrate, the NC deepest are kept (same rule as the oracle).
+template <int NC>
+__device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int lane) {
   int nhit = 0;
   for (int base = 0; base < m.npair; base += WAVE) {
     const int p = base + lane;
     float dist = 0, pos[3], nrm[3];
     bool hit = (p < m.npair) && narrow(s, m, p, dist, pos, nrm);
     const uint64_t mask = __ballot(hit);
-    const int before = __popcll(mask & ((1ull << lane) - 1ull));
-    const int slot = nhit + before;
+    const int slot = nhit + __popcll(mask & ((1ull << lane) - 1ull));
     if (hit) {
-      if (slot < NCMAX) store_contact(s, m, slot, p, dist, pos, nrm);
-      if (slot < WAVE) { s.hit_dist[slot] = dist; s.hit_pair[slot] = p; }
+      if (slot < NC) store_contact(s, m, slot, p, dist, pos, nrm);
+      if (slot < WAVE) { s.x.a.hit_dist[slot] = dist; s.x.a.hit_pair[slot] = p; }
     }
     nhit += __popcll(mask);
   }
-  if (lane == 0) { s.nhit = nhit; s.ncon = nhit < NCMAX ? nhit : NCMAX; }
-  if (nhit > NCMAX) {  // rare: keep the NCMAX deepest among the first WAVE hits, in pair order
+  if (lane == 0) { s.nhit = nhit; s.ncon = nhit < NC ? nhit : NC; }
+  if (nhit > NC) {  // rare: keep the NC deepest among the first WAVE hits, in pair order
     SYNC();
     const int nh = nhit < WAVE ? nhit : WAVE;
-    float myd = lane < nh ? s.hit_dist[lane] : 0.0f;
+    const float myd = lane < nh ? s.x.a.hit_dist[lane] : 0.0f;
     int rank = 0;
     for (int c = 0; c < nh; c++) {
-      float dc = s.hit_dist[c];
+      const float dc = s.x.a.hit_dist[c];
       rank += (dc < myd || (dc == myd && c < lane)) ? 1 : 0;
     }
-    const bool keep = lane < nh && rank < NCMAX;
+    const bool keep = lane < nh && rank < NC;
     const uint64_t km = __ballot(keep);
     const int slot = __popcll(km & ((1ull << lane) - 1ull));
-    int p = lane < nh ? s.hit_pair[lane] : 0;
+    const int p = lane < nh ? s.x.a.hit_pair[lane] : 0;
     SYNC();
     if (keep) {
       float dist, pos[3], nrm[3];
@@ -351,105 +385,101 @@ __device__ void collision(Shared& s, const DevModel& m, int lane) {
   }
 }
 
-// RNE leg pass (mj_comVel + mj_rne): lane l in 0..3 walks base then leg l; writes cvel,
-// subtree-accumulated leg cfrc and (lane 0) the base's own cfrc.
-__device__ void rne_pass(Shared& s, const DevModel& m, int lane) {
+// RNE velocity/acceleration chain (mj_comVel + forward half of mj_rne): lanes 0..3 each
+// walk base -> leg l writing cvel and cacc of its links (lane 0 also the base).
+template <int NC>
+__device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int lane) {
   if (lane >= 4) return;
   float cv[6] = {0, 0, 0, 0, 0, 0}, ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
-  float cdd[6];
   for (int d = 0; d < 3; d++)
     for (int k = 0; k < 6; k++) cv[k] += s.cdof[d][k] * s.qvel[d];
-  float cddr[3][6];
-  for (int d = 0; d < 3; d++) cross_motion(cddr[d], cv, s.cdof[3 + d]);
+  float cdd[6];
+  for (int d = 0; d < 3; d++) {
+    cross_motion(cdd, cv, s.cdof[3 + d]);
+    for (int k = 0; k < 6; k++) ca[k] += cdd[k] * s.qvel[3 + d];
+  }
   for (int d = 0; d < 3; d++)
     for (int k = 0; k < 6; k++) cv[k] += s.cdof[3 + d][k] * s.qvel[3 + d];
-  for (int d = 0; d < 3; d++)
-    for (int k = 0; k < 6; k++) ca[k] += cddr[d][k] * s.qvel[3 + d];
-  float f1[6], f2[6], f3[6];
-  if (lane == 0) {
-    mul_inert_vec(f1, s.cinert[1], ca);
-    mul_inert_vec(f2, s.cinert[1], cv);
-    cross_force(f3, cv, f2);
-    for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv[k]; s.cfrc[1][k] = f1[k] + f3[k]; }
-  }
-  float fb[3][6];
+  if (lane == 0)
+    for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv[k]; s.x.a.cacc[1][k] = ca[k]; }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const int b = 2 + 3 * lane + k, d = 6 + 3 * lane + k;
     cross_motion(cdd, cv, s.cdof[d]);
     const float qd = s.qvel[d];
     for (int c = 0; c < 6; c++) { cv[c] += s.cdof[d][c] * qd; ca[c] += cdd[c] * qd; }
-    mul_inert_vec(f1, s.cinert[b], ca);
-    mul_inert_vec(f2, s.cinert[b], cv);
-    cross_force(f3, cv, f2);
-    for (int c = 0; c < 6; c++) { fb[k][c] = f1[c] + f3[c]; s.cvel[b][c] = cv[c]; }
+    for (int c = 0; c < 6; c++) { s.cvel[b][c] = cv[c]; s.x.a.cacc[b][c] = ca[c]; }
   }
-  for (int c = 0; c < 6; c++) {
-    fb[1][c] += fb[2][c];
-    fb[0][c] += fb[1][c];
+}
+
+// body forces cinert*cacc + cvel x* (cinert*cvel), lanes 1..13 (one body each)
+template <int NC>
+__device__ __forceinline__ void rne_body_forces(Shared<NC>& s, int lane) {
+  if (lane >= 1 && lane < NB) {
+    float f1[6], f2[6], f3[6];
+    mul_inert_vec(f1, s.cinert[lane], s.x.a.cacc[lane]);
+    mul_inert_vec(f2, s.cinert[lane], s.cvel[lane]);
+    cross_force(f3, s.cvel[lane], f2);
+    for (int k = 0; k < 6; k++) s.x.a.cacc[lane][k] = f1[k] + f3[k];  // cfrc, in place
   }
-#pragma unroll
-  for (int k = 0; k < 3; k++)
-    for (int c = 0; c < 6; c++) s.cfrc[2 + 3 * lane + k][c] = fb[k][c];
 }
 
 // composite inertia of body b's subtree times cdof d (for M), lanes < NV
-__device__ void crb_times_cdof(Shared& s, const DevModel& m, int lane) {
+template <int NC>
+__device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m, int lane) {
   if (lane >= NV) return;
   const int b = m.dof_body[lane];
+  const int first = b == 1 ? 1 : b, last = b == 1 ? NB - 1 : 2 + 3 * ((b - 2) / 3) + 2;
   float crb[10];
   for (int k = 0; k < 10; k++) crb[k] = 0;
-  if (b == 1) {
-    for (int bb = 1; bb < NB; bb++)
-      for (int k = 0; k < 10; k++) crb[k] += s.cinert[bb][k];
-  } else {
-    const int last = 2 + 3 * ((b - 2) / 3) + 2;
-    for (int bb = b; bb <= last; bb++)
-      for (int k = 0; k < 10; k++) crb[k] += s.cinert[bb][k];
-  }
-  mul_inert_vec(s.F[lane], crb, s.cdof[lane]);
+  for (int bb = first; bb <= last; bb++)
+    for (int k = 0; k < 10; k++) crb[k] += s.cinert[bb][k];
+  mul_inert_vec(s.x.a.F[lane], crb, s.cdof[lane]);
 }
 
 // ------------------------------------------------------------------------------------
-// register LDL^T: lane i (< NV) holds row i; returns L_ik (k<i) in a[k], D_i in dd
+// register LDL^T: lane i (< NV) holds row i; returns L_ik (k<i) in a[k], 1/D_i in dinv
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dd, int lane) {
+__device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int lane) {
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    float dk = fmaxf(rlane(a[k], k), MINVAL);
-    dd = (lane == k) ? dk : dd;
-    const float lik = a[k] / dk;
+    const float dk = fmaxf(rlane(a[k], k), MINVAL);
+    const float ik = frcp(dk);
+    dinv = (lane == k) ? ik : dinv;
+    const float lik = a[k] * ik;
 #pragma unroll
     for (int j = k + 1; j < NV; ++j) a[j] -= lik * rlane(a[k], j);
     a[k] = (lane > k) ? lik : a[k];
   }
 }
-// solve L D L^T x = b; x = b_i on entry (lane i).  Uses s.L for the transposed factor.
-__device__ __forceinline__ float ldl_solve(Shared& s, const float (&a)[NV], float dd, float x, int lane) {
+// solve L D L^T x = b; x = b_i on entry (lane i).  Uses s.x.L for the transposed factor.
+template <int NC>
+__device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int lane) {
   const int li = lane < NV ? lane : NV - 1;
 #pragma unroll
   for (int k = 0; k < NV; ++k)
-    if (k < lane && lane < NV) s.L[lane][k] = a[k];
+    if (k < lane && lane < NV) s.x.L[lane][k] = a[k];
 #pragma unroll
   for (int k = 0; k < NV - 1; ++k) {
     const float yk = rlane(x, k);
     x = (lane > k) ? x - a[k] * yk : x;
   }
-  x = x / dd;
+  x = x * dinv;
   SYNC();
   float col[NV];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) col[k] = s.L[k][li];
+  for (int k = 1; k < NV; ++k) col[k] = s.x.L[k][li];
 #pragma unroll
   for (int k = NV - 1; k > 0; --k) {
     const float xk = rlane(x, k);
     x = (lane < k) ? x - col[k] * xk : x;
   }
-  return x;
+  return x;  // callers SYNC before s.x is rewritten
 }
 
 // J row r dotted with x (LDS vector)
-__device__ __forceinline__ float row_dot(const Shared& s, int r, const float* x) {
+template <int NC>
+__device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float* x) {
   if (r < NFR) return x[6 + r];
   if (r < NFR + s.nl) {
     const int i = r - NFR;
@@ -463,21 +493,38 @@ __device__ __forceinline__ float row_dot(const Shared& s, int r, const float* x)
   return a + sg * s.con_mu[c] * b;
 }
 
+// index drawn by jax.random.choice(p) from u = uniform(key): searchsorted_left(cumsum(p), cumsum[-1]*(1-u))
+__device__ __forceinline__ int choice_from_uniform(const float* dist, int n, float u) {
+  float total = 0.0f;
+  for (int i = 0; i < n; i++) total += dist[i];
+  const float r = total * (1.0f - u);
+  float acc = 0.0f;
+  int li = 0;
+  for (int i = 0; i < n; i++) {
+    acc += dist[i];
+    li += (acc < r) ? 1 : 0;
+  }
+  return li < n ? li : n - 1;
+}
+
 // ------------------------------------------------------------------------------------
-// one physics substep (mj_step): forward + Newton + Euler.  `integrate` = 0 for reset
+// one physics substep (mj_step): forward + Newton + Euler.  `integrate` = false for reset
 // (mj_forward only).  Must be called by all 64 lanes.
 // ------------------------------------------------------------------------------------
-__device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) {
+template <int NC>
+__device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int lane, bool integrate) {
   kinematics(s, m, lane);
   SYNC();
+  PHASE(0);
   com_pos(s, m, lane);
   SYNC();
-  // ---- phase 3: CRB*cdof, RNE, collision, actuation/passive, limit rows ----
+  PHASE(1);
+  // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
   crb_times_cdof(s, m, lane);
-  rne_pass(s, m, lane);
+  rne_chain(s, m, lane);
   collision(s, m, lane);
   {
-    // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle
+    // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
     bool act = false;
     float value = 0;
     int j = 0;
@@ -504,15 +551,13 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
       s.efc_aref[r] = -m.lim_b[j] * (sg * s.qvel[dof]) - m.lim_k[j] * imp * (value - m.lim_margin[j]);
     }
     if (lane == 0) s.nl = __popcll(mask);
-    // frictionloss rows
-    if (lane < NFR) {
+    if (lane < NFR) {  // dof frictionloss rows (R, b precomputed: pos = 0)
       const int dof = 6 + lane;
       s.efc_R[lane] = m.fr_R[dof];
       s.efc_D[lane] = 1.0f / m.fr_R[dof];
       s.efc_aref[lane] = -m.fr_b[dof] * s.qvel[dof];
     }
-    // actuation + passive
-    if (lane < NU) {
+    if (lane < NU) {  // actuation (affine PD + force clamp)
       const int d = m.act_dof[lane];
       float ctrl = s.ctrl[lane];
       if (m.act_ctrllimited[lane]) ctrl = fminf(fmaxf(ctrl, m.act_crange[lane][0]), m.act_crange[lane][1]);
@@ -528,47 +573,48 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
     if (lane < 6) s.qfrc_act[lane] = 0.0f;
   }
   SYNC();
-  // ---- phase 4: M entries, qfrc_bias/smooth, contact Jacobians ----
+  PHASE(2);
+  // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
   for (int p = lane; p < m.nmpair; p += WAVE) {
     const int i = m.mp_i[p], j = m.mp_j[p];
     float v = 0;
-    for (int k = 0; k < 6; k++) v += s.cdof[j][k] * s.F[i][k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) v += s.cdof[j][k] * s.x.a.F[i][k];
     if (i == j) v += m.dof_armature[i];
     s.M[i][j] = v;
     s.M[j][i] = v;
   }
-  if (lane < NV) {
-    const int b = m.dof_body[lane];
-    float cf[6];
-    for (int k = 0; k < 6; k++) cf[k] = s.cfrc[b][k];
-    if (b == 1)
-      for (int l = 0; l < 4; l++)
-        for (int k = 0; k < 6; k++) cf[k] += s.cfrc[2 + 3 * l][k];
-    float bias = 0;
-    for (int k = 0; k < 6; k++) bias += s.cdof[lane][k] * cf[k];
-    s.qfrc_bias[lane] = bias;
-    s.qfrc_smooth[lane] = -m.dof_damping[lane] * s.qvel[lane] - bias + s.qfrc_act[lane];
-  }
+  rne_body_forces(s, lane);
   const int ncon = s.ncon;
   for (int it = lane; it < ncon * NV; it += WAVE) {
     const int c = it / NV, i = it - c * NV;
     const int p = s.con_pair[c];
     const int b1 = m.cg_body[m.pair_g1[p]], b2 = m.cg_body[m.pair_g2[p]];
     const uint32_t bit = 1u << i;
-    float off[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
-    float jp[3] = {0, 0, 0};
+    const float off[3] = {s.x.a.con_pos[c][0] - s.com[0], s.x.a.con_pos[c][1] - s.com[1], s.x.a.con_pos[c][2] - s.com[2]};
     const float* cd = s.cdof[i];
-    float cr[3];
+    float cr[3], jp[3];
     cross3(cr, cd, off);
     const float w = ((m.body_dofmask[b2] & bit) ? 1.0f : 0.0f) - ((m.body_dofmask[b1] & bit) ? 1.0f : 0.0f);
     for (int k = 0; k < 3; k++) jp[k] = w * (cd[3 + k] + cr[k]);
-    const float* fr = s.con_frame[c];
+    const float* fr = s.x.a.con_frame[c];
     s.Jc[c][0][i] = fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2];
     s.Jc[c][1][i] = fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2];
     s.Jc[c][2][i] = fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2];
   }
   SYNC();
-  // ---- phase 5: contact edge rows (R, D, aref) ----
+  PHASE(3);
+  // ---- phase 5: qfrc_bias/smooth (subtree sums of body forces), contact edge rows ----
+  if (lane < NV) {
+    const int b = m.dof_body[lane];
+    const int first = b == 1 ? 1 : b, last = b == 1 ? NB - 1 : 2 + 3 * ((b - 2) / 3) + 2;
+    float cf[6] = {0, 0, 0, 0, 0, 0};
+    for (int bb = first; bb <= last; bb++)
+      for (int k = 0; k < 6; k++) cf[k] += s.x.a.cacc[bb][k];  // holds cfrc after phase 4
+    float bias = 0;
+    for (int k = 0; k < 6; k++) bias += s.cdof[lane][k] * cf[k];
+    s.qfrc_smooth[lane] = -m.dof_damping[lane] * s.qvel[lane] - bias + s.qfrc_act[lane];
+  }
   const int nl = s.nl;
   const int nefc = NFR + nl + 4 * ncon;
   for (int e = lane; e < 4 * ncon; e += WAVE) {
@@ -584,19 +630,21 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
     s.efc_D[r] = 1.0f / R;
     s.efc_aref[r] = -m.pair_b[p] * vel - m.pair_k[p] * imp * (dist - m.pair_margin[p]);
   }
+  SYNC();
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
   {
     const int li = lane < NV ? lane : NV - 1;
-    float a[NV], dd = 1.0f;
+    float a[NV], dinv = 1.0f;
 #pragma unroll
     for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
-    ldl_rows(a, dd, lane);
-    const float x = ldl_solve(s, a, dd, s.qfrc_smooth[li], lane);
+    ldl_rows(a, dinv, lane);
+    const float x = ldl_solve(s, a, dinv, s.qfrc_smooth[li], lane);
     if (lane < NV) s.qacc_smooth[lane] = x;
   }
   SYNC();
+  PHASE(4);
 
-  // ---- phase 7: Newton solver, 1..iterations, warm-started ----
+  // ---- phase 7: Newton solver (mj_solNewton), warm-started ----
   // per-lane rows r0 = lane, r1 = lane + 64
   float Dr[2], Rr[2], ar[2], fl[2];
   bool valid[2], isfr[2];
@@ -610,7 +658,7 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
     ar[t] = valid[t] ? s.efc_aref[r] : 0.0f;
     fl[t] = (valid[t] && isfr[t]) ? m.fr_floss[6 + r] : 0.0f;
   }
-  // warm start: cost at qacc_warmstart vs qacc_smooth
+  // warm start: total cost at qacc_warmstart vs at qacc_smooth
   {
     float cws = 0, csm = 0;
 #pragma unroll
@@ -630,6 +678,7 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
     }
     if (lane < NV) {
       float ma = 0;
+#pragma unroll
       for (int j = 0; j < NV; j++) ma += s.M[lane][j] * s.qws[j];
       cws += 0.5f * (ma - s.qfrc_smooth[lane]) * (s.qws[lane] - s.qacc_smooth[lane]);
     }
@@ -639,34 +688,35 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
     if (lane < NV) s.qacc[lane] = use_smooth ? s.qacc_smooth[lane] : s.qws[lane];
   }
   SYNC();
+  PHASE(5);
   for (int iter = 0; iter < m.iterations; iter++) {
     // Ma, Jaref, constraint state/force
     float ma = 0;
     if (lane < NV) {
+#pragma unroll
       for (int j = 0; j < NV; j++) ma += s.M[lane][j] * s.qacc[j];
       s.Ma[lane] = ma;
     }
-    float jar[2], Dq[2];
+    float jar[2];
 #pragma unroll
     for (int t = 0; t < 2; t++) {
       jar[t] = 0;
-      Dq[t] = 0;
       if (!valid[t]) continue;
       const int r = lane + WAVE * t;
       const float x = row_dot(s, r, s.qacc) - ar[t];
       jar[t] = x;
-      float f;
+      float f, Dq = 0.0f;
       if (isfr[t]) {
         const float rf = Rr[t] * fl[t];
         if (x <= -rf) f = fl[t];
         else if (x >= rf) f = -fl[t];
-        else { f = -Dr[t] * x; Dq[t] = Dr[t]; }
+        else { f = -Dr[t] * x; Dq = Dr[t]; }
       } else {
         if (x >= 0) f = 0;
-        else { f = -Dr[t] * x; Dq[t] = Dr[t]; }
+        else { f = -Dr[t] * x; Dq = Dr[t]; }
       }
       s.efc_force[r] = f;
-      s.efc_D[r] = Dq[t];  // active D (0 when not quadratic) for the Hessian
+      s.efc_D[r] = Dq;  // active D (0 when not quadratic) for the Hessian
     }
     SYNC();
     // gradient, diagonal D per dof, contact Hessian blocks
@@ -699,14 +749,16 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
     }
     gauss = wave_sum(gauss);
     SYNC();
+    PHASE(6);
     // Hessian rows H = M + J' D J (registers), LDL^T, search = -H^-1 grad
     {
       const int li = lane < NV ? lane : NV - 1;
-      float a[NV], dd = 1.0f;
+      float a[NV], dinv = 1.0f;
 #pragma unroll
       for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
+      const float dD = s.dofD[li];
 #pragma unroll
-      for (int j = 0; j < NV; j++) a[j] += (j == li) ? s.dofD[li] : 0.0f;
+      for (int j = 0; j < NV; j++) a[j] += (j == li) ? dD : 0.0f;
       for (int c = 0; c < ncon; c++) {
         const float* G = s.con_G[c];
         const float jn = s.Jc[c][0][li], j1 = s.Jc[c][1][li], j2 = s.Jc[c][2][li];
@@ -716,16 +768,18 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
 #pragma unroll
         for (int j = 0; j < NV; j++) a[j] += w0 * s.Jc[c][0][j] + w1 * s.Jc[c][1][j] + w2 * s.Jc[c][2][j];
       }
-      ldl_rows(a, dd, lane);
-      const float x = ldl_solve(s, a, dd, s.grad[li], lane);
+      ldl_rows(a, dinv, lane);
+      const float x = ldl_solve(s, a, dinv, s.grad[li], lane);
       if (lane < NV) s.search[lane] = -x;
     }
     SYNC();
-    // line-search quadratics
+    PHASE(7);
+    // line-search quadratics (Gauss part) and search-direction norm
     float q1 = 0, q2 = 0, sn = 0;
     if (lane < NV) {
       const float sv = s.search[lane];
       float mv = 0;
+#pragma unroll
       for (int j = 0; j < NV; j++) mv += s.M[lane][j] * s.search[j];
       q1 = sv * (s.Ma[lane] - s.qfrc_smooth[lane]);
       q2 = 0.5f * sv * mv;
@@ -739,7 +793,7 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
 #pragma unroll
     for (int t = 0; t < 2; t++) jv[t] = valid[t] ? row_dot(s, lane + WAVE * t, s.search) : 0.0f;
     const float gtol = m.gtol_scale * sn;
-    // evaluate cost/derivatives at alpha
+    // cost and derivatives of the 1-D piecewise quadratic at alpha
     auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
       float t0 = 0, t1 = 0, t2 = 0;
 #pragma unroll
@@ -765,17 +819,18 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
       d0 = t1 + 2.0f * alpha * t2;
       d1 = fmaxf(2.0f * t2, MINVAL);
     };
+    // PrimalSearch-style exact line search (same control flow as the oracle)
     int evals = 0;
     const int maxit = m.ls_iterations;
     float alpha;
     {
-      float a0 = 0, c0, g0, h0;
-      eval(a0, c0, g0, h0);
+      float c0, g0, h0;
+      eval(0.0f, c0, g0, h0);
       evals++;
-      float a1 = a0 - g0 / h0, c1, g1, h1;
+      float a1 = -g0 / h0, c1, g1, h1;
       eval(a1, c1, g1, h1);
       evals++;
-      if (c0 < c1) { a1 = a0; c1 = c0; g1 = g0; h1 = h0; }
+      if (c0 < c1) { a1 = 0.0f; c1 = c0; g1 = g0; h1 = h0; }
       if (fabsf(g1) < gtol) {
         alpha = a1;
       } else {
@@ -792,31 +847,36 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
         if (done || evals >= maxit) {
           alpha = a1;
         } else {
-          // bracket [p2, p1]
+          // bracket [p2, p1]; candidates p1next, p2next (= p1 initially), midpoint
           float a2n = a1, c2n = c1, g2n = g1;
           float a1n = a1 - g1 / h1, c1n, g1n, h1n;
           eval(a1n, c1n, g1n, h1n);
           evals++;
-          float h2n = h1;
-          (void)h2n;
-          alpha = c1 < c2 ? a1 : a2;
           bool finished = false;
+          alpha = c1 < c2 ? a1 : a2;
           while (evals < maxit) {
             const float am = 0.5f * (a1 + a2);
             float cm, gm, hm;
             eval(am, cm, gm, hm);
             evals++;
-            float ca[3] = {a1n, a2n, am}, cc[3] = {c1n, c2n, cm}, cg[3] = {g1n, g2n, gm};
-            float ch[3] = {h1n, h1, hm};
-            int best = -1;
-            for (int i = 0; i < 3; i++)
-              if (fabsf(cg[i]) < gtol && (best < 0 || cc[i] < cc[best])) best = i;
-            if (best >= 0) { alpha = ca[best]; finished = true; break; }
-            bool up1 = false, up2 = false;
-            for (int i = 0; i < 3; i++) {
-              if (g1 * cg[i] > 0 && fabsf(cg[i]) < fabsf(g1)) { a1 = ca[i]; c1 = cc[i]; g1 = cg[i]; h1 = ch[i]; up1 = true; }
-              if (g2 * cg[i] > 0 && fabsf(cg[i]) < fabsf(g2)) { a2 = ca[i]; c2 = cc[i]; g2 = cg[i]; h2 = ch[i]; up2 = true; }
+            // converged candidate with the lowest cost (order: p1next, p2next, mid)
+            bool ok0 = fabsf(g1n) < gtol, ok1 = fabsf(g2n) < gtol, ok2 = fabsf(gm) < gtol;
+            if (ok0 || ok1 || ok2) {
+              float ba = ok0 ? a1n : (ok1 ? a2n : am), bc = ok0 ? c1n : (ok1 ? c2n : cm);
+              if (ok1 && c2n < bc) { ba = a2n; bc = c2n; }
+              if (ok2 && cm < bc) { ba = am; bc = cm; }
+              alpha = ba;
+              finished = true;
+              break;
             }
+            bool up1 = false, up2 = false;
+#define PP3_TIGHTEN(CA, CC, CG, CH)                                                          \
+  if (g1 * (CG) > 0 && fabsf(CG) < fabsf(g1)) { a1 = CA; c1 = CC; g1 = CG; h1 = CH; up1 = true; } \
+  if (g2 * (CG) > 0 && fabsf(CG) < fabsf(g2)) { a2 = CA; c2 = CC; g2 = CG; h2 = CH; up2 = true; }
+            PP3_TIGHTEN(a1n, c1n, g1n, h1n)
+            PP3_TIGHTEN(a2n, c2n, g2n, h1)
+            PP3_TIGHTEN(am, cm, gm, hm)
+#undef PP3_TIGHTEN
             if (!up1 && !up2) break;
             if (up1) { a1n = a1 - g1 / h1; eval(a1n, c1n, g1n, h1n); evals++; }
             if (up2) { float hh; a2n = a2 - g2 / h2; eval(a2n, c2n, g2n, hh); evals++; }
@@ -825,6 +885,7 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
         }
       }
     }
+    PHASE(8);
     if (alpha == 0.0f) break;
     if (lane < NV) s.qacc[lane] += alpha * s.search[lane];
     SYNC();
@@ -844,8 +905,8 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
   if (lane < 3) s.qpos[lane] += h * vn;
   if (lane >= 6 && lane < NV) s.qpos[lane + 1] += h * vn;
   if (lane == 3) {
-    float n = sqrtf(dot3(w, w));
-    if (n < MINVAL) { w[0] = 1; w[1] = 0; w[2] = 0; } else { w[0] /= n; w[1] /= n; w[2] /= n; }
+    const float n = sqrtf(dot3(w, w));
+    if (n < MINVAL) { w[0] = 1; w[1] = 0; w[2] = 0; } else { const float in = 1.0f / n; w[0] *= in; w[1] *= in; w[2] *= in; }
     float qr[4], q[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
     axisangle2quat(qr, w, h * n);
     normalize4(q);
@@ -853,18 +914,19 @@ __device__ void substep(Shared& s, const DevModel& m, int lane, bool integrate) 
     for (int k = 0; k < 4; k++) s.qpos[3 + k] = q[k];
   }
   SYNC();
+  PHASE(9);
 }
 
 // ------------------------------------------------------------------------------------
 // environment helpers
 // ------------------------------------------------------------------------------------
-__device__ void load_params(Shared& s, const DevModel& m, const float* dr, int lane) {
+template <int NC>
+__device__ __forceinline__ void load_params(Shared<NC>& s, const DevModel& m, const float* dr, int lane) {
   if (lane < NB) {
-    const float* src = dr;
-    s.mass[lane] = src ? src[PP3_DR_MASS + lane] : m.body_mass[lane];
+    s.mass[lane] = dr ? dr[PP3_DR_MASS + lane] : m.body_mass[lane];
     for (int k = 0; k < 3; k++) {
-      s.inertia[lane][k] = src ? src[PP3_DR_INERTIA + 3 * lane + k] : m.body_inertia[lane][k];
-      s.ipos[lane][k] = (src && lane == 1) ? src[PP3_DR_BASE_IPOS + k] : m.body_ipos[lane][k];
+      s.inertia[lane][k] = dr ? dr[PP3_DR_INERTIA + 3 * lane + k] : m.body_inertia[lane][k];
+      s.ipos[lane][k] = (dr && lane == 1) ? dr[PP3_DR_BASE_IPOS + k] : m.body_ipos[lane][k];
     }
   }
   if (lane == 0) {
@@ -873,25 +935,43 @@ __device__ void load_params(Shared& s, const DevModel& m, const float* dr, int l
     s.kp = dr ? dr[PP3_DR_KP] : 0.0f;
     s.kd = dr ? dr[PP3_DR_KD] : 0.0f;
   }
-  // zero M once (its sparsity pattern is fixed)
+  // zero M once per launch (its sparsity pattern is fixed)
   for (int i = lane; i < NV * (NV + 1); i += WAVE) (&s.M[0][0])[i] = 0.0f;
 }
 
-// sample_command (environment.py:246-272): uses lanes 0..7, writes out[3] in LDS
-__device__ void sample_command(Shared& s, const DevModel& m, Key rng, float* out, int lane) {
+__device__ __forceinline__ Key bcast_key(Key k, int l) {
+  return Key{(uint32_t)__builtin_amdgcn_readlane((int)k.a, l), (uint32_t)__builtin_amdgcn_readlane((int)k.b, l)};
+}
+
+// sample_lagged_value on one buffer row in HBM (utils.py:34-69): push `v` to the front of
+// row[0..n), return the value now at column li.  Register-staged (read all, then write).
+__device__ __forceinline__ float push_lagged(float* row, int n, float v, int li) {
+  float old[PP3_MAX_LAG];
+#pragma unroll
+  for (int l = 0; l < PP3_MAX_LAG; l++) old[l] = l < n ? row[l] : 0.0f;
+  float out = v;
+#pragma unroll
+  for (int l = 0; l < PP3_MAX_LAG; l++) {
+    const float nv = l == 0 ? v : old[l - 1];
+    if (l < n) row[l] = nv;
+    out = (l == li) ? nv : out;
+  }
+  return out;
+}
+
+// sample_command (environment.py:246-272): lanes 0..6 draw, lane 0 writes out[3]
+__device__ __forceinline__ void sample_command(const DevModel& m, Key rng, float* out, int lane) {
   const int part = m.partitionable;
   float u = 0;
   if (lane < 3) {
-    Key k = split_i(rng, 6, 1 + lane, part);
+    const Key k = split_i(rng, 6, 1 + lane, part);
     const float lo = lane == 0 ? m.cmd_x[0] : lane == 1 ? m.cmd_y[0] : m.cmd_w[0];
     const float hi = lane == 0 ? m.cmd_x[1] : lane == 1 ? m.cmd_y[1] : m.cmd_w[1];
     u = uniform_i(k, 1, 0, lo, hi, part);
   } else if (lane == 3) {
-    Key k = split_i(rng, 6, 4, part);
-    u = uniform_i(k, 1, 0, 0.0f, 1.0f, part);
+    u = uniform_i(split_i(rng, 6, 4, part), 1, 0, 0.0f, 1.0f, part);
   } else if (lane < 7) {
-    Key k = split_i(rng, 6, 5, part);
-    u = uniform_i(k, 3, lane - 4, -m.stand_thr, m.stand_thr, part);
+    u = uniform_i(split_i(rng, 6, 5, part), 3, lane - 4, -m.stand_thr, m.stand_thr, part);
   }
   const bool zero = rlane(u, 3) < m.zero_cmd_p;
   const float c0 = rlane(u, 0), c1 = rlane(u, 1), c2 = rlane(u, 2);
@@ -903,124 +983,119 @@ __device__ void sample_command(Shared& s, const DevModel& m, Key rng, float* out
   }
 }
 
-// sample_body_orientation (environment.py:274-298)
-__device__ void sample_orientation(Shared& s, const DevModel& m, Key rng, float* out, int lane) {
+// sample_body_orientation (environment.py:274-298), brax math.euler_to_quat (degrees)
+__device__ __forceinline__ void sample_orientation(const DevModel& m, Key rng, float* out, int lane) {
   const int part = m.partitionable;
   float u = 0;
-  if (lane < 2) {
-    Key k = split_i(rng, 3, 1 + lane, part);
-    u = uniform_i(k, 1, 0, -1.0f, 1.0f, part);
-  }
+  if (lane < 2) u = uniform_i(split_i(rng, 3, 1 + lane, part), 1, 0, -1.0f, 1.0f, part);
   const float pitch = rlane(u, 0) * m.max_pitch;
   const float roll = rlane(u, 1) * m.max_roll;
   if (lane == 0) {
     const float pi = m.pi_f;
-    float v[3] = {roll, pitch, 0.0f};
-    float c1 = cosf(v[0] * pi / 360.0f), c2 = cosf(v[1] * pi / 360.0f), c3 = cosf(v[2] * pi / 360.0f);
-    float s1 = sinf(v[0] * pi / 360.0f), s2 = sinf(v[1] * pi / 360.0f), s3 = sinf(v[2] * pi / 360.0f);
-    float q[4] = {c1 * c2 * c3 - s1 * s2 * s3, s1 * c2 * c3 + c1 * s2 * s3, c1 * s2 * c3 - s1 * c2 * s3,
-                  c1 * c2 * s3 + s1 * s2 * c3};
+    const float c1 = cosf(roll * pi / 360.0f), c2 = cosf(pitch * pi / 360.0f), c3 = 1.0f;
+    const float s1 = sinf(roll * pi / 360.0f), s2 = sinf(pitch * pi / 360.0f), s3 = 0.0f;
+    const float q[4] = {c1 * c2 * c3 - s1 * s2 * s3, s1 * c2 * c3 + c1 * s2 * s3, c1 * s2 * c3 - s1 * c2 * s3,
+                        c1 * c2 * s3 + s1 * s2 * c3};
     float r[3];
     b_rotate(r, m.des_z, q);
     out[0] = r[0]; out[1] = r[1]; out[2] = r[2];
   }
 }
 
-// _get_obs (environment.py:485-543): consumes st rng, pushes IMU buffer, writes s.o[36]
-__device__ void get_obs(Shared& s, const DevModel& m, int lane) {
+// _get_obs (environment.py:485-543): consumes the st rng, pushes the IMU buffer (HBM row
+// gimu = [6][Li]), writes s.x.e.o[36]
+template <int NC>
+__device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int lane) {
   const int part = m.partitionable;
-  Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
-  if (lane < 6) {
-    Key k = split_i(rng, 6, lane, part);
-    s.keys[lane][0] = k.a;
-    s.keys[lane][1] = k.b;
+  const Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
+  const Key kl = split_i(rng, 6, lane < 6 ? lane : 0, part);  // lane i holds split(rng, 6)[i]
+  const Key k0 = bcast_key(kl, 0), ka = bcast_key(kl, 1), kg = bcast_key(kl, 2);
+  const Key km = bcast_key(kl, 3), kla = bcast_key(kl, 4), ki = bcast_key(kl, 5);
+  // noise draws: 0-2 ang, 3-5 grav, 6-17 motor, 18-29 last act, 30 imu choice
+  if (lane < 31) {
+    const Key kk = lane < 3 ? ka : lane < 6 ? kg : lane < 18 ? km : lane < 30 ? kla : ki;
+    const int cnt = lane < 6 ? 3 : lane < 30 ? 12 : 1;
+    const int idx = lane < 3 ? lane : lane < 6 ? lane - 3 : lane < 18 ? lane - 6 : lane < 30 ? lane - 18 : 0;
+    const float scale = lane < 3 ? m.n_ang : lane < 6 ? m.n_grav : lane < 18 ? m.n_motor : lane < 30 ? m.n_act : 1.0f;
+    const float lo = lane < 30 ? -1.0f : 0.0f;
+    const float v = uniform_i(kk, cnt, idx, lo, 1.0f, part);
+    s.x.e.u[lane] = lane < 30 ? v * scale : v;
   }
   SYNC();
-  // noise draws: 0-2 ang(k1), 3-5 grav(k2), 6-17 motor(k3), 18-29 last act(k4), 30 imu choice(k5)
-  if (lane < 3) s.u[lane] = uniform_i(key_of(s, 1), 3, lane, -1.0f, 1.0f, part) * m.n_ang;
-  else if (lane < 6) s.u[lane] = uniform_i(key_of(s, 2), 3, lane - 3, -1.0f, 1.0f, part) * m.n_grav;
-  else if (lane < 18) s.u[lane] = uniform_i(key_of(s, 3), 12, lane - 6, -1.0f, 1.0f, part) * m.n_motor;
-  else if (lane < 30) s.u[lane] = uniform_i(key_of(s, 4), 12, lane - 18, -1.0f, 1.0f, part) * m.n_act;
-  else if (lane == 30) s.u[30] = uniform_i(key_of(s, 5), 1, 0, 0.0f, 1.0f, part);
-  SYNC();
-  if (lane == 0) {
+  if (lane < 6) {  // one IMU channel per lane
     float inv[4] = {1, 0, 0, 0}, angl[3] = {0, 0, 0};
     if (m.use_imu) {
       inv[0] = s.xquat[1][0]; inv[1] = -s.xquat[1][1]; inv[2] = -s.xquat[1][2]; inv[3] = -s.xquat[1][3];
       b_rotate(angl, s.cvel[1], inv);
     }
-    float g0[3] = {0, 0, -1}, g[3];
+    const float g0[3] = {0, 0, -1};
+    float g[3];
     b_rotate(g, g0, inv);
-    for (int k = 0; k < 3; k++) g[k] += s.u[3 + k];
+    for (int k = 0; k < 3; k++) g[k] += s.x.e.u[3 + k];
     const float gn = sqrtf(dot3(g, g));
-    float imu[6];
-    for (int k = 0; k < 3; k++) { imu[k] = angl[k] + s.u[k]; imu[3 + k] = g[k] / gn; }
-    const int Li = m.Li;
-    float* ib = s.st + m.imu_off;
-    for (int r = 0; r < 6; r++) {
-      for (int l = Li - 1; l > 0; l--) ib[r * Li + l] = ib[r * Li + l - 1];
-      ib[r * Li] = imu[r];
-    }
-    // jax.random.choice with p (searchsorted left on the f32 cumsum)
-    float cum[PP3_MAX_LAG], acc = 0.0f;
-    for (int i = 0; i < Li; i++) { acc += m.imu_lat_dist[i]; cum[i] = acc; }
-    const float r = cum[Li - 1] * (1.0f - s.u[30]);
-    int li = 0;
-    while (li < Li && cum[li] < r) li++;
-    for (int k = 0; k < 6; k++) s.o[k] = fminf(fmaxf(ib[k * Li + li], -100.0f), 100.0f);
-    s.st[PP3_S_RNG] = __uint_as_float(s.keys[0][0]);
-    s.st[PP3_S_RNG + 1] = __uint_as_float(s.keys[0][1]);
+    const float v = lane < 3 ? angl[lane] + s.x.e.u[lane] : g[lane - 3] / gn;
+    const int li = choice_from_uniform(m.imu_lat_dist, m.Li, s.x.e.u[30]);
+    const float lagged = push_lagged(gimu + lane * m.Li, m.Li, v, li);
+    s.x.e.o[lane] = fminf(fmaxf(lagged, -100.0f), 100.0f);
   }
-  if (lane < 3) {
-    s.o[6 + lane] = fminf(fmaxf(s.st[PP3_S_COMMAND + lane], -100.0f), 100.0f);
-    s.o[9 + lane] = fminf(fmaxf(s.st[PP3_S_DESIRED_Z + lane], -100.0f), 100.0f);
+  if (lane == 6) {
+    s.st[PP3_S_RNG] = __uint_as_float(k0.a);
+    s.st[PP3_S_RNG + 1] = __uint_as_float(k0.b);
   }
-  if (lane < 12) {
-    const float a = s.qpos[7 + lane] - m.default_pose[lane] + s.u[6 + lane];
-    const float b = s.st[PP3_S_LAST_ACT + lane] + s.u[18 + lane];
-    s.o[12 + lane] = fminf(fmaxf(a, -100.0f), 100.0f);
-    s.o[24 + lane] = fminf(fmaxf(b, -100.0f), 100.0f);
+  if (lane >= 8 && lane < 11) {
+    const int k = lane - 8;
+    s.x.e.o[6 + k] = fminf(fmaxf(s.st[PP3_S_COMMAND + k], -100.0f), 100.0f);
+    s.x.e.o[9 + k] = fminf(fmaxf(s.st[PP3_S_DESIRED_Z + k], -100.0f), 100.0f);
+  }
+  if (lane >= 16 && lane < 28) {
+    const int j = lane - 16;
+    const float a = s.qpos[7 + j] - m.default_pose[j] + s.x.e.u[6 + j];
+    const float b = s.st[PP3_S_LAST_ACT + j] + s.x.e.u[18 + j];
+    s.x.e.o[12 + j] = fminf(fmaxf(a, -100.0f), 100.0f);
+    s.x.e.o[24 + j] = fminf(fmaxf(b, -100.0f), 100.0f);
   }
   SYNC();
 }
 
-__device__ void write_obs(Shared& s, const DevModel& m, const float* obs_in, float* obs_out, int lane) {
-  const int H = m.H;
-  const int nmove = PP3_OBS_DIM * (H - 1);
+template <int NC>
+__device__ __forceinline__ void write_obs(Shared<NC>& s, const DevModel& m, const float* obs_in, float* obs_out,
+                                          int lane) {
+  const int nmove = PP3_OBS_DIM * (m.H - 1);
   float tmp[OBS_MOVE];
 #pragma unroll
   for (int t = 0; t < OBS_MOVE; t++) {
     const int k = lane + WAVE * t;
     tmp[t] = (k < nmove && obs_in) ? obs_in[k] : 0.0f;
   }
-  SYNC();
 #pragma unroll
   for (int t = 0; t < OBS_MOVE; t++) {
     const int k = lane + WAVE * t;
     if (k < nmove) obs_out[PP3_OBS_DIM + k] = tmp[t];
   }
-  if (lane < PP3_OBS_DIM) obs_out[lane] = s.o[lane];
+  if (lane < PP3_OBS_DIM) obs_out[lane] = s.x.e.o[lane];
 }
 
-__device__ void write_pipeline(Shared& s, const DevModel& m, float* p, int lane) {
+template <int NC>
+__device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int lane) {
   for (int i = lane; i < PP3_PIPE_STRIDE; i += WAVE) {
     float v = 0.0f;
-    if (i < PP3_P_XQUAT) { int b = 1 + i / 3, k = i % 3; v = s.xpos[b][k]; }
-    else if (i < PP3_P_XD_VEL) { int q = i - PP3_P_XQUAT, b = 1 + q / 4, k = q % 4; v = s.xquat[b][k]; }
+    if (i < PP3_P_XQUAT) { const int b = 1 + i / 3, k = i % 3; v = s.xpos[b][k]; }
+    else if (i < PP3_P_XD_VEL) { const int q = i - PP3_P_XQUAT, b = 1 + q / 4, k = q % 4; v = s.xquat[b][k]; }
     else if (i < PP3_P_XD_ANG) {
-      int q = i - PP3_P_XD_VEL, b = 1 + q / 3, k = q % 3;
-      float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]}, cr[3];
+      const int q = i - PP3_P_XD_VEL, b = 1 + q / 3, k = q % 3;
+      const float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]};
+      float cr[3];
       cross3(cr, s.cvel[b], off);
       v = s.cvel[b][3 + k] + cr[k];
-    } else if (i < PP3_P_SITE_XPOS) { int q = i - PP3_P_XD_ANG, b = 1 + q / 3, k = q % 3; v = s.cvel[b][k]; }
-    else if (i < PP3_P_QFRC_ACT) { int q = i - PP3_P_SITE_XPOS, f = q / 3, k = q % 3; v = s.site_xpos[m.feet_site[f]][k]; }
+    } else if (i < PP3_P_SITE_XPOS) { const int q = i - PP3_P_XD_ANG, b = 1 + q / 3, k = q % 3; v = s.cvel[b][k]; }
+    else if (i < PP3_P_QFRC_ACT) { const int q = i - PP3_P_SITE_XPOS, f = q / 3, k = q % 3; v = s.foot_xpos[f][k]; }
     else if (i < PP3_P_QACC) v = s.qfrc_act[i - PP3_P_QFRC_ACT];
     else if (i < PP3_P_NCON) v = s.qacc[i - PP3_P_QACC];
     else if (i == PP3_P_NCON) v = (float)s.ncon;
-    else if (i < PP3_P_CON_GEOM) { int c = i - PP3_P_CON_DIST; v = c < s.ncon ? s.con_dist[c] : 0.0f; }
+    else if (i < PP3_P_CON_GEOM) { const int c = i - PP3_P_CON_DIST; v = c < s.ncon ? s.con_dist[c] : 0.0f; }
     else if (i < PP3_P_SUBTREE_COM) {
-      int q = i - PP3_P_CON_GEOM, c = q / 2;
-      if (c < s.ncon) { int pp = s.con_pair[c]; v = (float)m.cg_id[(q & 1) ? m.pair_g2[pp] : m.pair_g1[pp]]; }
+      const int q = i - PP3_P_CON_GEOM, c = q / 2;
+      if (c < s.ncon) { const int pp = s.con_pair[c]; v = (float)m.cg_id[(q & 1) ? m.pair_g2[pp] : m.pair_g1[pp]]; }
     } else if (i < PP3_P_SUBTREE_COM + 3) v = s.com[i - PP3_P_SUBTREE_COM];
     p[i] = v;
   }
@@ -1031,20 +1106,21 @@ __device__ void write_pipeline(Shared& s, const DevModel& m, float* p, int lane)
 // ------------------------------------------------------------------------------------
 struct StepArgs {
   const DevModel* m;
-  float* state;      // [N][stride]
-  const float* obs_in;
-  float* obs_out;    // [N][36H]
+  float* state;          // [N][stride]
+  const float* obs_in;   // [N][36H]
+  float* obs_out;        // [N][36H]
   const float* actions;  // [N][12]
   float* reward;
   float* done;
-  float* metrics;    // [N][19]
-  const float* dr;   // [N][62] or null
-  float* pipe;       // [N][PIPE] or null
+  float* metrics;        // [N][19]
+  const float* dr;       // [N][62] or null
+  float* pipe;           // [N][PIPE] or null
   int N;
 };
 
-__global__ __launch_bounds__(WAVE) void env_step_kernel(StepArgs a) {
-  __shared__ Shared s;
+template <int NC>
+__global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArgs a) {
+  __shared__ Shared<NC> s;
   const int env = blockIdx.x;
   const int lane = threadIdx.x;
   if (env >= a.N) return;
@@ -1052,79 +1128,83 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(StepArgs a) {
   const int stride = m.stride;
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;
-  for (int i = lane; i < stride; i += WAVE) s.st[i] = gst[i];
+#ifdef PP3_PHASE_PROF
+  if (lane < 16) s.prof[lane] = 0;
+  if (lane == 0) s.prof_t = __builtin_amdgcn_s_memtime();
+#endif
+  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) s.st[i] = gst[i];
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, lane);
   SYNC();
   if (lane < NQ) s.qpos[lane] = s.st[PP3_S_QPOS + lane];
   if (lane < NV) { s.qvel[lane] = s.st[PP3_S_QVEL + lane]; s.qws[lane] = s.st[PP3_S_QACC_WS + lane]; }
-  // ---- prologue: rng split, kick, action latency ----
-  Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
-  if (lane < 5) {
-    Key k = split_i(rng, 5, lane, part);
-    s.keys[lane][0] = k.a;
-    s.keys[lane][1] = k.b;
-  }
-  SYNC();
+  // ---- prologue: rng split (environment.py:349), kick (:352-356), action latency (:359-365) ----
+  const Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
+  const Key kl = split_i(rng, 5, lane < 5 ? lane : 0, part);  // lane i holds split(rng, 5)[i]
+  const Key k_new = bcast_key(kl, 0), cmd_key = bcast_key(kl, 1);
+  const Key kkick = bcast_key(kl, 2), kbern = bcast_key(kl, 3), klat = bcast_key(kl, 4);
   float u = 0;
-  if (lane < 2) u = uniform_i(key_of(s, 2), 2, lane, -1.0f, 1.0f, part);
-  else if (lane < 4) u = uniform_i(key_of(s, lane == 2 ? 3 : 4), 1, 0, 0.0f, 1.0f, part);
+  if (lane < 4) {
+    const Key kk = lane < 2 ? kkick : (lane == 2 ? kbern : klat);
+    u = uniform_i(kk, lane < 2 ? 2 : 1, lane < 2 ? lane : 0, lane < 2 ? -1.0f : 0.0f, 1.0f, part);
+  }
   const float bern = rlane(u, 2) < m.kick_p ? 1.0f : 0.0f;
   const float kick0 = rlane(u, 0) * m.kick_vel * bern, kick1 = rlane(u, 1) * m.kick_vel * bern;
-  const Key cmd_key = key_of(s, 1);
+  const int li = choice_from_uniform(m.lat_dist, m.La, rlane(u, 3));
   if (lane == 0) {
     s.qvel[0] += kick0;
     s.qvel[1] += kick1;
     s.st[PP3_S_KICK] = kick0;
     s.st[PP3_S_KICK + 1] = kick1;
-    s.st[PP3_S_RNG] = __uint_as_float(s.keys[0][0]);
-    s.st[PP3_S_RNG + 1] = __uint_as_float(s.keys[0][1]);
+    s.st[PP3_S_RNG] = __uint_as_float(k_new.a);
+    s.st[PP3_S_RNG + 1] = __uint_as_float(k_new.b);
   }
-  {
-    float cum[PP3_MAX_LAG], acc = 0.0f;
-    const int La = m.La;
-    for (int i = 0; i < La; i++) { acc += m.lat_dist[i]; cum[i] = acc; }
-    const float r = cum[La - 1] * (1.0f - rlane(u, 3));
-    int li = 0;
-    while (li < La && cum[li] < r) li++;
-    if (lane < NU) {
-      const float act = a.actions[(size_t)env * NU + lane];
-      float* ab = s.st + PP3_S_ACT_BUF + lane * La;
-      for (int l = La - 1; l > 0; l--) ab[l] = ab[l - 1];
-      ab[0] = act;
-      const float t = m.default_pose[lane] + ab[li] * m.action_scale;
-      s.ctrl[lane] = fminf(fmaxf(t, m.jlo[lane]), m.jhi[lane]);
-    }
+  const float* act_env = a.actions + (size_t)env * NU;
+  if (lane < NU) {
+    const float lagged = push_lagged(gst + PP3_S_ACT_BUF + lane * m.La, m.La, act_env[lane], li);
+    const float t = m.default_pose[lane] + lagged * m.action_scale;
+    s.ctrl[lane] = fminf(fmaxf(t, m.jlo[lane]), m.jhi[lane]);
   }
   SYNC();
-  // ---- physics ----
-  for (int f = 0; f < m.n_frames; f++) substep(s, m, lane, true);
+  PHASE(10);
+  // ---- physics: n_frames x mj_step (environment.py:366) ----
+  for (int f = 0; f < m.n_frames; f++) {
+    const DevModel* mp = a.m;
+    int ln = lane;
+    // opaque per iteration: keep model loads and lane-derived addresses inside the substep
+    // (hoisting them out of the loop costs more registers than recomputing them)
+    asm volatile("" : "+s"(mp), "+v"(ln));
+    substep(s, *mp, ln, true);
+  }
   if (lane < NQ) s.st[PP3_S_QPOS + lane] = s.qpos[lane];
   if (lane < NV) { s.st[PP3_S_QVEL + lane] = s.qvel[lane]; s.st[PP3_S_QACC_WS + lane] = s.qws[lane]; }
   SYNC();
   // ---- observation ----
-  get_obs(s, m, lane);
+  get_obs(s, m, gst + m.imu_off, lane);
   write_obs(s, m, a.obs_in + (size_t)env * PP3_OBS_DIM * m.H, a.obs_out + (size_t)env * PP3_OBS_DIM * m.H, lane);
+  PHASE(11);
   // ---- brax x/xd, feet, done, collisions ----
   if (lane >= 1 && lane < NB) {
     const int b = lane;
-    float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]}, cr[3];
+    const float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]};
+    float cr[3];
     cross3(cr, s.cvel[b], off);
-    for (int k = 0; k < 3; k++) { s.xdv[b][k] = s.cvel[b][3 + k] + cr[k]; s.xda[b][k] = s.cvel[b][k]; }
+    for (int k = 0; k < 3; k++) { s.x.e.xdv[b][k] = s.cvel[b][3 + k] + cr[k]; s.x.e.xda[b][k] = s.cvel[b][k]; }
   }
   if (lane >= 16 && lane < 20) {
     const int f = lane - 16;
-    const float cz = s.site_xpos[m.feet_site[f]][2] - m.foot_radius;
+    const float cz = s.foot_xpos[f][2] - m.foot_radius;
     const int last = s.st[PP3_S_LAST_CONTACT + f] != 0.0f;
     const int c = cz < 1e-3f;
-    s.contact[f] = c;
-    s.filt_mm[f] = c | last;
-    s.filt_cm[f] = (cz < 3e-2f) | last;
-    s.first[f] = (s.st[PP3_S_AIR_TIME + f] > 0.0f && (c | last)) ? 1.0f : 0.0f;
+    s.x.e.contact[f] = c;
+    s.x.e.filt_mm[f] = c | last;
+    s.x.e.filt_cm[f] = (cz < 3e-2f) | last;
+    s.x.e.first[f] = (s.st[PP3_S_AIR_TIME + f] > 0.0f && (c | last)) ? 1.0f : 0.0f;
     s.st[PP3_S_AIR_TIME + f] += m.dt;
   }
   if (lane == 20) {
     const int tb = m.torso_body;
-    float up[3] = {0, 0, 1}, ru[3];
+    const float up[3] = {0, 0, 1};
+    float ru[3];
     b_rotate(ru, up, s.xquat[tb]);
     int d = dot3(ru, up) < m.cos_term_angle;
     for (int j = 0; j < 12; j++) {
@@ -1132,7 +1212,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(StepArgs a) {
       if (s.qpos[7 + j] > m.jhi[j]) d = 1;
     }
     if (s.xpos[tb][2] < m.term_z) d = 1;
-    s.done = d;
+    s.x.e.done = d;
   }
   if (lane == 21) {
     float knee = 0, bodyc = 0;
@@ -1143,13 +1223,13 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(StepArgs a) {
       for (int i = 0; i < m.n_knee_geoms; i++) knee += (ga == m.knee_geoms[i] || gb == m.knee_geoms[i]) ? 1.0f : 0.0f;
       for (int i = 0; i < m.n_torso_geoms; i++) bodyc += (ga == m.torso_geoms[i] || gb == m.torso_geoms[i]) ? 1.0f : 0.0f;
     }
-    s.knee = knee;
-    s.bodyc = bodyc;
+    s.x.e.knee = knee;
+    s.x.e.bodyc = bodyc;
   }
   SYNC();
   // ---- rewards (rewards.py), one term per lane ----
   if (lane < PP3_NREWARD) {
-    float inv[4] = {s.xquat[1][0], -s.xquat[1][1], -s.xquat[1][2], -s.xquat[1][3]};
+    const float inv[4] = {s.xquat[1][0], -s.xquat[1][1], -s.xquat[1][2], -s.xquat[1][3]};
     const float cmd0 = s.st[PP3_S_COMMAND], cmd1 = s.st[PP3_S_COMMAND + 1], cmd2 = s.st[PP3_S_COMMAND + 2];
     const float cn = sqrtf(cmd0 * cmd0 + cmd1 * cmd1 + cmd2 * cmd2);
     const float sig = m.sigma;
@@ -1157,26 +1237,28 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(StepArgs a) {
     switch (lane) {
       case PP3_REWARD_TRACKING_LIN_VEL: {
         float lv[3];
-        b_rotate(lv, s.xdv[1], inv);
+        b_rotate(lv, s.x.e.xdv[1], inv);
         const float e = (cmd0 - lv[0]) * (cmd0 - lv[0]) + (cmd1 - lv[1]) * (cmd1 - lv[1]);
         v = expf(-e / sig);
       } break;
       case PP3_REWARD_TRACKING_ANG_VEL: {
         float av[3];
-        b_rotate(av, s.xda[1], inv);
+        b_rotate(av, s.x.e.xda[1], inv);
         v = expf(-(cmd2 - av[2]) * (cmd2 - av[2]) / sig);
       } break;
       case PP3_REWARD_TRACKING_ORIENTATION: {
-        float z0[3] = {0, 0, 1}, wz[3];
+        const float z0[3] = {0, 0, 1};
+        float wz[3];
         b_rotate(wz, z0, inv);
         float e = 0;
         for (int k = 0; k < 3; k++) e += (wz[k] - s.st[PP3_S_DESIRED_Z + k]) * (wz[k] - s.st[PP3_S_DESIRED_Z + k]);
         v = expf(-e / sig);
       } break;
-      case PP3_REWARD_LIN_VEL_Z: v = s.xdv[1][2] * s.xdv[1][2]; break;
-      case PP3_REWARD_ANG_VEL_XY: v = s.xda[1][0] * s.xda[1][0] + s.xda[1][1] * s.xda[1][1]; break;
+      case PP3_REWARD_LIN_VEL_Z: v = s.x.e.xdv[1][2] * s.x.e.xdv[1][2]; break;
+      case PP3_REWARD_ANG_VEL_XY: v = s.x.e.xda[1][0] * s.x.e.xda[1][0] + s.x.e.xda[1][1] * s.x.e.xda[1][1]; break;
       case PP3_REWARD_ORIENTATION: {
-        float z0[3] = {0, 0, 1}, ru[3];
+        const float z0[3] = {0, 0, 1};
+        float ru[3];
         b_rotate(ru, z0, s.xquat[1]);
         v = ru[0] * ru[0] + ru[1] * ru[1];
       } break;
@@ -1194,7 +1276,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(StepArgs a) {
         break;
       case PP3_REWARD_ACTION_RATE:
         for (int j = 0; j < 12; j++) {
-          const float d = a.actions[(size_t)env * NU + j] - s.st[PP3_S_LAST_ACT + j];
+          const float d = act_env[j] - s.st[PP3_S_LAST_ACT + j];
           v += d * d;
         }
         break;
@@ -1213,60 +1295,64 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(StepArgs a) {
         }
         break;
       case PP3_REWARD_FEET_AIR_TIME:
-        for (int f = 0; f < 4; f++) v += (s.st[PP3_S_AIR_TIME + f] - 0.1f) * s.first[f];
+        for (int f = 0; f < 4; f++) v += (s.st[PP3_S_AIR_TIME + f] - 0.1f) * s.x.e.first[f];
         v *= (cn > 0.05f) ? 1.0f : 0.0f;
         break;
       case PP3_REWARD_FOOT_SLIP:
         for (int f = 0; f < 4; f++) {
           const int b = m.lower_leg_body[f];
-          const float* sp = s.site_xpos[m.feet_site[f]];
-          float off[3] = {sp[0] - s.xpos[b][0], sp[1] - s.xpos[b][1], sp[2] - s.xpos[b][2]}, cr[3];
-          cross3(cr, s.xda[b], off);
-          const float vx = s.xdv[b][0] + cr[0], vy = s.xdv[b][1] + cr[1];
-          v += (vx * vx + vy * vy) * (s.filt_cm[f] ? 1.0f : 0.0f);
+          const float* sp = s.foot_xpos[f];
+          const float off[3] = {sp[0] - s.xpos[b][0], sp[1] - s.xpos[b][1], sp[2] - s.xpos[b][2]};
+          float cr[3];
+          cross3(cr, s.x.e.xda[b], off);
+          const float vx = s.x.e.xdv[b][0] + cr[0], vy = s.x.e.xdv[b][1] + cr[1];
+          v += (vx * vx + vy * vy) * (s.x.e.filt_cm[f] ? 1.0f : 0.0f);
         }
         break;
       case PP3_REWARD_TERMINATION:
-        v = (s.done && (int)s.st[PP3_S_STEP] < m.term_step) ? 1.0f : 0.0f;
+        v = (s.x.e.done && (int)s.st[PP3_S_STEP] < m.term_step) ? 1.0f : 0.0f;
         break;
-      case PP3_REWARD_KNEE_COLLISION: v = s.knee; break;
-      case PP3_REWARD_BODY_COLLISION: v = s.bodyc; break;
+      case PP3_REWARD_KNEE_COLLISION: v = s.x.e.knee; break;
+      case PP3_REWARD_BODY_COLLISION: v = s.x.e.bodyc; break;
     }
-    s.rw[lane] = v * m.scales[lane];
+    s.x.e.rw[lane] = v * m.scales[lane];
   }
   SYNC();
   // ---- state management (environment.py:448-482) ----
   int stepc = (int)s.st[PP3_S_STEP] + 1;
   const bool resample = stepc > m.resample_step;
-  const bool isdone = s.done != 0;
+  const bool isdone = s.x.e.done != 0;
   if (lane == 0) {
     float sum = 0.0f;
-    for (int k = 0; k < PP3_NREWARD; k++) sum += s.rw[k];
-    const float rew = fminf(fmaxf(sum * m.dt, 0.0f), 10000.0f);
-    a.reward[env] = rew;
+    for (int k = 0; k < PP3_NREWARD; k++) sum += s.x.e.rw[k];
+    a.reward[env] = fminf(fmaxf(sum * m.dt, 0.0f), 10000.0f);
     a.done[env] = isdone ? 1.0f : 0.0f;
     const int tb = m.torso_body;
-    float* met = a.metrics + (size_t)env * PP3_NMETRIC;
-    met[0] = sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
+    a.metrics[(size_t)env * PP3_NMETRIC] =
+        sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
   }
-  if (lane < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + lane] = s.rw[lane];
+  if (lane < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + lane] = s.x.e.rw[lane];
   if (lane < NU) {
-    s.st[PP3_S_LAST_ACT + lane] = a.actions[(size_t)env * NU + lane];
+    s.st[PP3_S_LAST_ACT + lane] = act_env[lane];
     s.st[PP3_S_LAST_VEL + lane] = s.qvel[6 + lane];
   }
   if (lane < 4) {
-    if (s.filt_mm[lane]) s.st[PP3_S_AIR_TIME + lane] = 0.0f;
-    s.st[PP3_S_LAST_CONTACT + lane] = s.contact[lane] ? 1.0f : 0.0f;
+    if (s.x.e.filt_mm[lane]) s.st[PP3_S_AIR_TIME + lane] = 0.0f;
+    s.st[PP3_S_LAST_CONTACT + lane] = s.x.e.contact[lane] ? 1.0f : 0.0f;
   }
   if (resample) {
-    sample_command(s, m, cmd_key, s.st + PP3_S_COMMAND, lane);
-    sample_orientation(s, m, cmd_key, s.st + PP3_S_DESIRED_Z, lane);
+    sample_command(m, cmd_key, s.st + PP3_S_COMMAND, lane);
+    sample_orientation(m, cmd_key, s.st + PP3_S_DESIRED_Z, lane);
   }
   if (isdone || resample) stepc = 0;
   if (lane == 0) s.st[PP3_S_STEP] = (float)stepc;
   if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, lane);
   SYNC();
-  for (int i = lane; i < stride; i += WAVE) gst[i] = s.st[i];
+  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) gst[i] = s.st[i];
+  PHASE(12);
+#ifdef PP3_PHASE_PROF
+  if (lane < 13) atomicAdd(&g_prof[lane], (unsigned long long)s.prof[lane]);
+#endif
 }
 
 struct ResetArgs {
@@ -1283,38 +1369,33 @@ struct ResetArgs {
   int N;
 };
 
-__global__ __launch_bounds__(WAVE) void env_reset_kernel(ResetArgs a) {
-  __shared__ Shared s;
+template <int NC>
+__global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_reset_kernel(ResetArgs a) {
+  __shared__ Shared<NC> s;
   const int env = blockIdx.x;
   const int lane = threadIdx.x;
   if (env >= a.N) return;
   if (a.mask && !a.mask[env]) return;
   const DevModel& m = *a.m;
   const int part = m.partitionable;
+  float* gst = a.state + (size_t)env * m.stride;
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, lane);
-  for (int i = lane; i < m.stride; i += WAVE) s.st[i] = 0.0f;
+  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) s.st[i] = 0.0f;
+  for (int i = PP3_S_ACT_BUF + lane; i < m.stride; i += WAVE) gst[i] = 0.0f;  // latency buffers
   SYNC();
   const Key rng{a.keys[2 * env], a.keys[2 * env + 1]};
-  if (lane < 4) {
-    Key k = split_i(rng, 4, lane, part);
-    s.keys[lane][0] = k.a;
-    s.keys[lane][1] = k.b;
-  }
-  SYNC();
-  const Key k0 = key_of(s, 0), kcmd = key_of(s, 1), kori = key_of(s, 2), kpos = key_of(s, 3);
-  // randomize_qpos (domain_randomization.py:188-210)
+  const Key kl = split_i(rng, 4, lane < 4 ? lane : 0, part);
+  const Key k0 = bcast_key(kl, 0), kcmd = bcast_key(kl, 1), kori = bcast_key(kl, 2), kpos = bcast_key(kl, 3);
+  // randomize_qpos (domain_randomization.py:188-210) on the home keyframe with default_pose
   float u = 0;
-  if (lane < 3) {
-    Key kp = split_i(kpos, 3, 1, part);
-    u = uniform_i(kp, 3, lane, m.start_lo[lane], m.start_hi[lane], part);
-  } else if (lane == 3) {
-    Key ky = split_i(kpos, 3, 2, part);
-    u = uniform_i(ky, 1, 0, -m.pi_f, m.pi_f, part);
+  if (lane < 4) {
+    const Key kk = split_i(kpos, 3, lane < 3 ? 1 : 2, part);
+    u = lane < 3 ? uniform_i(kk, 3, lane, m.start_lo[lane], m.start_hi[lane], part)
+                 : uniform_i(kk, 1, 0, -m.pi_f, m.pi_f, part);
   }
   const float yaw = rlane(u, 3);
   if (lane < NQ) {
-    float q = m.key_qpos[lane];
-    if (lane >= 7) q = m.default_pose[lane - 7];
+    float q = lane >= 7 ? m.default_pose[lane - 7] : m.key_qpos[lane];
     if (lane < 3) q = u;
     if (lane == 3) q = cosf(yaw / 2.0f);
     if (lane == 4 || lane == 5) q = 0.0f;
@@ -1324,26 +1405,24 @@ __global__ __launch_bounds__(WAVE) void env_reset_kernel(ResetArgs a) {
   if (lane < NV) { s.qvel[lane] = 0.0f; s.qws[lane] = 0.0f; }
   if (lane < NU) s.ctrl[lane] = 0.0f;
   SYNC();
-  substep(s, m, lane, false);  // pipeline_init: mjx.forward
+  substep(s, m, lane, false);  // pipeline_init: mjx.forward at (q, qd=0, ctrl=0)
   if (lane < NQ) s.st[PP3_S_QPOS + lane] = s.qpos[lane];
   if (lane < NV) { s.st[PP3_S_QVEL + lane] = 0.0f; s.st[PP3_S_QACC_WS + lane] = s.qws[lane]; }
   if (lane == 0) {
     s.st[PP3_S_RNG] = __uint_as_float(k0.a);
     s.st[PP3_S_RNG + 1] = __uint_as_float(k0.b);
   }
+  sample_command(m, kcmd, s.st + PP3_S_COMMAND, lane);
+  sample_orientation(m, kori, s.st + PP3_S_DESIRED_Z, lane);
+  if (lane < m.Li) gst[m.imu_off + 5 * m.Li + lane] = -1.0f;  // initial_imu_buffer gravity row
   SYNC();
-  sample_command(s, m, kcmd, s.st + PP3_S_COMMAND, lane);
-  sample_orientation(s, m, kori, s.st + PP3_S_DESIRED_Z, lane);
-  if (lane < m.Li) s.st[m.imu_off + 5 * m.Li + lane] = -1.0f;
-  SYNC();
-  get_obs(s, m, lane);
+  get_obs(s, m, gst + m.imu_off, lane);
   write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, lane);
   if (lane == 0) { a.reward[env] = 0.0f; a.done[env] = 0.0f; }
   if (lane < PP3_NMETRIC) a.metrics[(size_t)env * PP3_NMETRIC + lane] = 0.0f;
   if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, lane);
   SYNC();
-  float* gst = a.state + (size_t)env * m.stride;
-  for (int i = lane; i < m.stride; i += WAVE) gst[i] = s.st[i];
+  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) gst[i] = s.st[i];
 }
 
 struct PhysArgs {
@@ -1356,8 +1435,9 @@ struct PhysArgs {
   int N;
 };
 
-__global__ __launch_bounds__(WAVE) void physics_kernel(PhysArgs a) {
-  __shared__ Shared s;
+template <int NC>
+__global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void physics_kernel(PhysArgs a) {
+  __shared__ Shared<NC> s;
   const int env = blockIdx.x;
   const int lane = threadIdx.x;
   if (env >= a.N) return;
@@ -1368,7 +1448,14 @@ __global__ __launch_bounds__(WAVE) void physics_kernel(PhysArgs a) {
   if (lane < NV) { s.qvel[lane] = gst[PP3_S_QVEL + lane]; s.qws[lane] = gst[PP3_S_QACC_WS + lane]; }
   if (lane < NU) s.ctrl[lane] = a.ctrl[(size_t)env * NU + lane];
   SYNC();
-  for (int i = 0; i < a.nsteps; i++) substep(s, m, lane, true);
+  for (int i = 0; i < a.nsteps; i++) {
+    const DevModel* mp = a.m;
+    int ln = lane;
+    // opaque per iteration: keep model loads and lane-derived addresses inside the substep
+    // (hoisting them out of the loop costs more registers than recomputing them)
+    asm volatile("" : "+s"(mp), "+v"(ln));
+    substep(s, *mp, ln, true);
+  }
   if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, lane);
   if (lane < NQ) gst[PP3_S_QPOS + lane] = s.qpos[lane];
   if (lane < NV) { gst[PP3_S_QVEL + lane] = s.qvel[lane]; gst[PP3_S_QACC_WS + lane] = s.qws[lane]; }
@@ -1407,6 +1494,7 @@ struct pp3_env {
   int dr_on;
   float* pipe;
   int pipe_on;
+  int nc;  // contact cap (kernel template): 8 on flat terrain, 16 with obstacle geoms
   float* action;
   hipEvent_t ev0, ev1;
 };
@@ -1474,6 +1562,9 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
         return set_err(PP3_ERR_MODEL, "legs must be 4 serial chains of 3 hinge bodies");
     }
   if (mm->cone != PP3_CONE_PYRAMIDAL) return set_err(PP3_ERR_MODEL, "only pyramidal cones");
+  for (int j = 1; j < NJ; j++)
+    if (mm->jnt_pos[j][0] != 0 || mm->jnt_pos[j][1] != 0 || mm->jnt_pos[j][2] != 0)
+      return set_err(PP3_ERR_MODEL, "hinge anchors must coincide with body origins (jnt_pos = 0)");
   if (mm->eulerdamp) {
     for (int i = 0; i < NV; i++)
       if (mm->dof_damping[i] > 0) return set_err(PP3_ERR_MODEL, "eulerdamp with joint damping is not supported (xml:58 disables it)");
@@ -1560,7 +1651,7 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
       for (int k = 0; k < 3; k++) d->cg_pos[g][k] = (float)mm->cgeom_pos[g][k];
     } else {
       if (mm->cgeom_type[g] != PP3_GEOM_SPHERE) return set_err(PP3_ERR_MODEL, "moving collision geoms must be spheres");
-      if (nslot >= MAX_ROBOT_GEOM) return set_err(PP3_ERR_MODEL, "too many robot collision geoms");
+      if (nslot >= NROBOT_GEOM) return set_err(PP3_ERR_MODEL, "too many robot collision geoms (max 8)");
       d->cg_slot[g] = nslot;
       d->robot_geom[nslot++] = g;
       for (int k = 0; k < 3; k++) d->cg_pos[g][k] = (float)mm->cgeom_pos[g][k];
@@ -1692,7 +1783,8 @@ size_t pp3_struct_size(int which) {
   if (which == 0) return sizeof(pp3_model_t);
   if (which == 1) return sizeof(pp3_env_config_t);
   if (which == 2) return sizeof(DevModel);
-  if (which == 3) return sizeof(Shared);
+  if (which == 3) return sizeof(Shared<8>);
+  if (which == 4) return sizeof(Shared<16>);
   return 0;
 }
 
@@ -1716,6 +1808,16 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   e->N = num_envs;
   e->stride = hm.stride;
   e->H = hm.H;
+  {
+    int has_static_solid = 0;
+    for (int g = 0; g < model->ncgeom; g++)
+      if (model->cgeom_bodyid[g] == 0 && model->cgeom_type[g] != PP3_GEOM_PLANE) has_static_solid = 1;
+    e->nc = cfg->ncon_max > 0 ? cfg->ncon_max : (has_static_solid ? 16 : 8);
+    if (e->nc != 8 && e->nc != 16) {
+      delete e;
+      return set_err(PP3_ERR_ARG, "ncon_max must be 0 (auto), 8 or 16");
+    }
+  }
   const size_t N = (size_t)num_envs;
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   HIPCHK(hipMalloc(&e->dmodel, sizeof(DevModel)));
@@ -1773,7 +1875,8 @@ int pp3_reset(pp3_env_t* e, const uint32_t* keys_dev, const uint8_t* mask_dev, v
   a.dr = e->dr_on ? e->dr : nullptr;
   a.pipe = e->pipe_on ? e->pipe : nullptr;
   a.N = e->N;
-  hipLaunchKernelGGL(env_reset_kernel, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  if (e->nc == 8) hipLaunchKernelGGL(env_reset_kernel<8>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  else hipLaunchKernelGGL(env_reset_kernel<16>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
   return PP3_OK;
 }
@@ -1793,7 +1896,8 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   a.dr = e->dr_on ? e->dr : nullptr;
   a.pipe = e->pipe_on ? e->pipe : nullptr;
   a.N = e->N;
-  hipLaunchKernelGGL(env_step_kernel, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  else hipLaunchKernelGGL(env_step_kernel<16>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
   e->obs_cur ^= 1;
   return PP3_OK;
@@ -1825,7 +1929,8 @@ int pp3_physics_step(pp3_env_t* e, const float* ctrl_dev, int32_t nsteps, void* 
   a.pipe = e->pipe;
   a.nsteps = nsteps;
   a.N = e->N;
-  hipLaunchKernelGGL(physics_kernel, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  if (e->nc == 8) hipLaunchKernelGGL(physics_kernel<8>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  else hipLaunchKernelGGL(physics_kernel<16>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
   return PP3_OK;
 }
@@ -1912,6 +2017,22 @@ int pp3_fill_uniform(pp3_env_t* e, float* dev, int64_t count, uint32_t seed, uin
   hipLaunchKernelGGL(fill_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, stream_of(e, stream), dev, count, seed, ctr, lo, hi);
   HIPCHK(hipGetLastError());
   return PP3_OK;
+}
+
+int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset) {
+#ifdef PP3_PHASE_PROF
+  if (n > NPROF) n = NPROF;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_prof), sizeof(uint64_t) * n));
+  if (reset) {
+    unsigned long long z[NPROF] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+  }
+  return PP3_OK;
+#else
+  (void)host_out; (void)n; (void)reset;
+  return set_err(PP3_ERR_ARG, "pp3_phase_profile: library built without -DPP3_PHASE_PROF");
+#endif
 }
 
 int pp3_step_timed(pp3_env_t* e, const float* actions_dev, int64_t action_stride, int32_t nsteps,

@@ -88,7 +88,7 @@ class EnvConfig(C.Structure):
         ("feet_site", _a(i32, NFOOT)), ("lower_leg_body", _a(i32, NFOOT)),
         ("n_upper_leg_geoms", i32), ("upper_leg_geoms", _a(i32, 16)),
         ("n_torso_geoms", i32), ("torso_geoms", _a(i32, 8)),
-        ("rng_partitionable", i32), ("pad0", i32),
+        ("rng_partitionable", i32), ("ncon_max", i32),
         ("latency_dist", _a(d, MAX_LAG)), ("imu_latency_dist", _a(d, MAX_LAG)),
         ("action_scale", d), ("default_pose", _a(d, NU)), ("joint_lower", _a(d, NU)),
         ("joint_upper", _a(d, NU)), ("desired_abduction", _a(d, 4)),

@@ -11,7 +11,7 @@ import os
 from . import _abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpupper_hip.so")
+LIB_PATH = os.environ.get("PP3_LIB_PATH") or os.path.join(_HERE, "libpupper_hip.so")
 _lib = None
 
 
@@ -56,10 +56,11 @@ def load() -> C.CDLL:
     L.pp3_memcpy_d2d.argtypes = [vp, vp, sz, vp]
     L.pp3_fill_uniform.argtypes = [vp, vp, i64, C.c_uint32, C.c_uint32, C.c_float, C.c_float, vp]
     L.pp3_step_timed.argtypes = [vp, vp, i64, i32, C.POINTER(C.c_float)]
+    L.pp3_phase_profile.argtypes = [C.POINTER(C.c_uint64), i32, i32]
     for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
                  "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
-                 "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed"):
+                 "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile"):
         getattr(L, name).restype = C.c_int
     if L.pp3_abi_version() != _abi.ABI_VERSION:
         raise PupperHipError("ABI version mismatch between libpupper_hip.so and pupperv3_mjx/_abi.py")
@@ -80,7 +81,7 @@ EXPORTED_SYMBOLS = (
     "pp3_num_envs", "pp3_state_stride", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
     "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
-    "pp3_fill_uniform", "pp3_step_timed",
+    "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
 )
 
 

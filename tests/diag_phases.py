@@ -1,0 +1,47 @@
+"""Diagnostic: per-phase shader-clock breakdown of env_step_kernel (PP3_PHASE_PROF build).
+
+PP3_LIB_PATH=pupperv3-mjx_amd/pupperv3_mjx/libpupper_hip_prof.so python tests/diag_phases.py
+Read the SHARES, not the absolute time (the stamps serialise the phases they bracket).
+"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pupperv3-mjx_amd")]
+os.environ.setdefault("PP3_LIB_PATH", os.path.join(ROOT, "pupperv3-mjx_amd", "pupperv3_mjx", "libpupper_hip_prof.so"))
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+from pupperv3_mjx import MODEL_XML, _abi, _lib  # noqa: E402
+from pupperv3_mjx.environment import PupperV3Env, make_keys  # noqa: E402
+
+NAMES = ["kinematics", "com/cinert/cdof", "crb*cdof+rne+collision+rows", "M+bias+contactJ", "edge rows+LDL(M)",
+         "warmstart", "newton update+grad", "hessian+LDL+solve", "line search", "integrate",
+         "prologue", "obs", "rewards+state"]
+
+
+def main():
+    E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    steps = 20
+    env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=False)
+    env.reset(make_keys(0, E))
+    L = env._L
+    acts = _lib.DeviceBuffer((steps + 5) * E * 48)
+    _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, (steps + 5) * E * 12, 1, 0, -1.0, 1.0, None))
+    ms = C.c_float()
+    _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, 5, C.byref(ms)))
+    buf = (C.c_uint64 * 16)()
+    _lib.check(L.pp3_phase_profile(buf, 16, 1))
+    _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + 5 * E * 48), E * 12, steps, C.byref(ms)))
+    _lib.check(L.pp3_phase_profile(buf, 16, 1))
+    v = np.array(buf[:13], dtype=np.float64)
+    tot = v.sum()
+    print(f"E={E}: {ms.value / steps:.3f} ms/step (prof build); cycles per env-step per env: {tot / (E * steps):.0f}")
+    for n, x in zip(NAMES, v):
+        print(f"  {n:32s} {100 * x / tot:6.2f}%   {x / (E * steps):10.0f} cyc/env-step")
+
+
+if __name__ == "__main__":
+    main()
