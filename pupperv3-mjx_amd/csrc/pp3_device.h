@@ -110,15 +110,35 @@ struct DevModel {
 __device__ __forceinline__ float rlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+// Wave-wide reductions on the DPP network (no LDS round trips): butterfly
+// within each 16-lane row (quad_perm, row_half_mirror, row_mirror), then
+// row_bcast:15 / row_bcast:31 fold the four rows into lane 63, which is
+// read back as a wave-uniform scalar.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float v, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
+                                                    ROWMASK, 0xF, false));
+}
+__device__ __forceinline__ float lane63(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-  return v;
+  v += dpp_f<0xB1, 0xF>(v, 0.0f);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xF>(v, 0.0f);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xF>(v, 0.0f);  // row_half_mirror
+  v += dpp_f<0x140, 0xF>(v, 0.0f);  // row_mirror
+  v += dpp_f<0x142, 0xA>(v, 0.0f);  // row_bcast:15 -> rows 1,3
+  v += dpp_f<0x143, 0xC>(v, 0.0f);  // row_bcast:31 -> rows 2,3
+  return lane63(v);
 }
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, WAVE));
-  return v;
+  v = fminf(v, dpp_f<0xB1, 0xF>(v, v));
+  v = fminf(v, dpp_f<0x4E, 0xF>(v, v));
+  v = fminf(v, dpp_f<0x141, 0xF>(v, v));
+  v = fminf(v, dpp_f<0x140, 0xF>(v, v));
+  v = fminf(v, dpp_f<0x142, 0xA>(v, v));
+  v = fminf(v, dpp_f<0x143, 0xC>(v, v));
+  return lane63(v);
 }
 __device__ __forceinline__ void quat2mat(const float q[4], float R[9]) {
   float w = q[0], x = q[1], y = q[2], z = q[3];

@@ -39,7 +39,8 @@ def oracle_physics(model, qpos, qvel, qws, ctrl, nsteps, precision="f64", dr=Non
 
 def record_to_oracle_state(rec_f32: np.ndarray) -> np.ndarray:
     """Device f32 record (rng bit-cast) -> oracle double record (rng as integer values)."""
-    out = rec_f32.astype(np.float64)
+    with np.errstate(invalid="ignore"):
+        out = rec_f32.astype(np.float64)
     out[..., _abi.S_RNG:_abi.S_RNG + 2] = rec_f32[..., _abi.S_RNG:_abi.S_RNG + 2].copy().view(np.uint32)
     return out
 
