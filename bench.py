@@ -122,8 +122,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
 
-    from pupperv3_mjx import MODEL_XML, _abi, _lib
-    from pupperv3_mjx.environment import PupperV3Env, make_keys
+    from pupperv3_mjx import MODEL_XML, _abi, _lib, sharding
+    from pupperv3_mjx.environment import PupperV3Env
 
     model_path = MODEL_XML
     if args.obstacles:
@@ -143,7 +143,7 @@ def main():
         from pupperv3_mjx import domain_randomization as dr, rng
         sysb, _ = dr.domain_randomize(env.sys, rng.split(rng.PRNGKey(1000 + rank), E))
         env.set_domain_randomization(sysb)
-    keys = make_keys(args.seed + 7919 * rank, E)
+    keys = sharding.shard_keys(args.seed, E * world, world, rank)  # global env ids, contiguous shards
     st = env.reset(keys)
     rec = st._record.copy()
     rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]
@@ -159,9 +159,9 @@ def main():
         _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, args.warmup, C.byref(ms)))
     gather_buf = None
     if args.gather and world > 1:
-        obs_ptr, obs_n = env.device_field(_abi.F_OBS)
-        local = torch.empty((E, obs_n + 2), device="cuda")
-        gather_buf = (local, torch.empty((world * E, obs_n + 2), device="cuda"))
+        obs_n = env.device_field(_abi.F_OBS)[1]
+        gather_buf = (torch.empty((E, obs_n), device="cuda"), torch.empty(E, device="cuda"),
+                      torch.empty(E, device="cuda"))
 
     def barrier():
         if world > 1:
@@ -177,14 +177,16 @@ def main():
         kernel_ms = ms.value
     else:
         kernel_ms = 0.0
-        local, full = gather_buf
+        obs_t, rew_t, done_t = gather_buf
         for i in range(args.steps):
             _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + (args.warmup + i) * E * 48), 0, 1,
                                         C.byref(ms)))
             kernel_ms += ms.value
-            obs_ptr, obs_n = env.device_field(_abi.F_OBS)
-            _lib.check(L.pp3_memcpy_d2d(C.c_void_p(local.data_ptr()), C.c_void_p(obs_ptr), E * obs_n * 4, None))
-            dist.all_gather_into_tensor(full, local)
+            env.synchronize()  # step ran on the handle's stream; copies + gather go on torch's (null) stream
+            for fid, t in ((_abi.F_OBS, obs_t), (_abi.F_REWARD, rew_t), (_abi.F_DONE, done_t)):
+                ptr, _ = env.device_field(fid)
+                _lib.check(L.pp3_memcpy_d2d(C.c_void_p(t.data_ptr()), C.c_void_p(ptr), t.numel() * 4, None))
+            sharding.gather_batch(obs_t, rew_t, done_t, E * world)
     env.synchronize()
     torch.cuda.synchronize()
     barrier()

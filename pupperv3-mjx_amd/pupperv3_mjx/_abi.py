@@ -16,6 +16,8 @@ S_QPOS, S_QVEL, S_QACC_WS, S_RNG = 0, 19, 37, 55
 S_LAST_ACT, S_LAST_VEL, S_COMMAND, S_DESIRED_Z = 57, 69, 81, 84
 S_AIR_TIME, S_LAST_CONTACT, S_KICK, S_STEP, S_ACT_BUF = 87, 91, 95, 97, 98
 
+GEOM_PLANE, GEOM_SPHERE, GEOM_BOX = 0, 2, 6
+
 F_STATE, F_OBS, F_REWARD, F_DONE, F_METRICS, F_DR, F_PIPELINE, F_ACTION = range(8)
 
 P_XPOS, P_XQUAT, P_XD_VEL, P_XD_ANG = 0, 39, 91, 130

@@ -94,3 +94,24 @@ def random_physics_states(n, seed=0, mode="mixed"):
         qvel[i] = rs.normal(scale=0.3, size=18)
         ctrl[i] = np.array(DEFAULT_POSE) + rs.uniform(-0.5, 0.5, 12)
     return qpos, qvel, np.zeros((n, 18)), ctrl
+
+
+def states_on_boxes(model, n, seed=0, z_range=(0.15, 0.175)):
+    """Seeded (qpos, qvel, qacc_ws, ctrl) with the robot straddling the obstacle walls
+    (obstacles.py boxes: 2 cm wide, 6 m long, top at z=0.02) so sphere-box contacts occur."""
+    rs = np.random.RandomState(seed)
+    boxes = [g for g in range(model.ncgeom) if model.cgeom_type[g] == _abi.GEOM_BOX]
+    assert boxes, "model has no box geoms"
+    qpos, qvel, qws, ctrl = random_physics_states(n, seed=seed, mode="stand")
+    for i in range(n):
+        g = boxes[rs.randint(len(boxes))]
+        c = np.array(model.cgeom_pos[g][:])
+        w, x, y, z = model.cgeom_quat[g][:]
+        # box local y axis (the 6 m length) in world
+        ay = np.array([2 * (x * y - w * z), 1 - 2 * (x * x + z * z), 2 * (y * z + w * x)])
+        t = rs.uniform(-2.5, 2.5)
+        p = c + t * ay + np.array([rs.uniform(-0.12, 0.12), rs.uniform(-0.12, 0.12), 0.0])
+        qpos[i, 0:2] = p[:2]
+        qpos[i, 2] = rs.uniform(*z_range)
+        qvel[i] *= 0.3
+    return qpos, qvel, qws, ctrl

@@ -1,0 +1,174 @@
+"""GPU edge cases through the C ABI vs the oracle: obstacle (sphere-box) contacts, contact-cap
+overflow ranking, masked reset, single-env / ragged batches, maximum history and latency lengths.
+
+Tolerances as in test_gpu_physics.py / test_gpu_env.py (fp32 kernel vs fp64/fp32 oracle):
+  physics  : |dqpos| <= 2e-5 per substep (or 5x the fp32 oracle's own error), |dqvel| <= 3e-3,
+             contact counts and contact geom pairs equal after one substep
+  env step : obs |d| <= 5e-3, reward |d| <= 1e-3, RNG words / command / step bit-exact
+"""
+import numpy as np
+import pytest
+
+import common
+import gpu_harness as G
+from oracle import oracle as O
+from pupperv3_mjx import _abi
+from pupperv3_mjx.environment import PupperV3Env, make_keys
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def box_path(require_gpu, tmp_path_factory):
+    return common.write_model(tmp_path_factory.mktemp("m"), 10)
+
+
+def _box_ids(model):
+    return {int(model.cgeom_id[g]) for g in range(model.ncgeom) if model.cgeom_type[g] == _abi.GEOM_BOX}
+
+
+def _contact_set(pipe):
+    n = int(pipe[_abi.P_NCON])
+    g = pipe[_abi.P_CON_GEOM:_abi.P_CON_GEOM + 2 * n].reshape(n, 2)
+    return sorted(map(tuple, g.astype(int).tolist()))
+
+
+def _physics_compare(env, m, qpos, qvel, qws, ctrl, nsteps, ncon_max=0):
+    gq, gv, _, gp = G.gpu_physics(env, qpos, qvel, qws, ctrl, nsteps)
+    oq, ov, op, fq, fv = [], [], [], [], []
+    for i in range(qpos.shape[0]):
+        q, v, _, p, _ = O.mj_step(m, qpos[i], qvel[i], qws[i], ctrl[i], nsteps=nsteps, ncon_max=ncon_max)
+        q32, v32, _, _, _ = O.mj_step(m, qpos[i], qvel[i], qws[i], ctrl[i], nsteps=nsteps, ncon_max=ncon_max,
+                                      precision="f32")
+        oq.append(q); ov.append(v); op.append(p); fq.append(q32); fv.append(v32)
+    oq, ov, op, fq, fv = map(np.array, (oq, ov, op, fq, fv))
+    assert np.all(np.isfinite(gq)) and np.all(np.isfinite(gv))
+    eq, ev = np.abs(gq - oq).max(), np.abs(gv - ov).max()
+    assert eq <= max(2e-5 * nsteps, 5 * np.abs(fq - oq).max()), eq
+    assert ev <= max(3e-3, 5 * np.abs(fv - ov).max()), ev
+    return gp, op
+
+
+@pytest.mark.parametrize("nsteps", [1, 3])
+def test_sphere_box_contact_parity(box_path, nsteps):
+    e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=64)
+    try:
+        m = e.sys_model.struct
+        assert e.config_struct.ncon_max == 0
+        qpos, qvel, qws, ctrl = common.states_on_boxes(m, 64, seed=nsteps)
+        gp, op = _physics_compare(e, m, qpos, qvel, qws, ctrl, nsteps)
+        if nsteps == 1:
+            boxes = _box_ids(m)
+            n_box = 0
+            for i in range(64):
+                gs, os_ = _contact_set(gp[i]), _contact_set(op[i])
+                assert gs == os_, (i, gs, os_)
+                n_box += sum(1 for a, b in gs if a in boxes or b in boxes)
+            assert n_box >= 16, n_box  # the states really exercise the sphere-box collider
+    finally:
+        e.close()
+
+
+def test_contact_cap_overflow_keeps_deepest(box_path):
+    """More penetrating pairs than the cap: the kernel and the oracle keep the same deepest set."""
+    e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=64, max_contacts=8)
+    try:
+        m = e.sys_model.struct
+        qpos, qvel, qws, ctrl = common.states_on_boxes(m, 64, seed=11, z_range=(0.085, 0.10))
+        qpos[:, 7:] = (np.array(common.DEFAULT_POSE) + np.tile([0, 0.0, 0.6, 0, 0.0, -0.6], 2)  # knees down
+                       + np.random.RandomState(12).uniform(-0.1, 0.1, size=(64, 12)))  # no exact depth ties
+        gp, op = _physics_compare(e, m, qpos, qvel, qws, ctrl, 1, ncon_max=8)
+        full = [O.mj_step(m, qpos[i], qvel[i], qws[i], ctrl[i], nsteps=1, ncon_max=16)[3] for i in range(64)]
+        overflow = sum(1 for p in full if p[_abi.P_NCON] > 8)
+        assert overflow >= 4, overflow
+        for i in range(64):
+            assert gp[i][_abi.P_NCON] == op[i][_abi.P_NCON] <= 8
+            assert _contact_set(gp[i]) == _contact_set(op[i]), i
+    finally:
+        e.close()
+
+
+def test_masked_reset_touches_only_masked_envs(box_path):
+    from pupperv3_mjx import _lib
+    n = 8
+    e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=n)
+    try:
+        st = e.reset(make_keys(0, n))
+        st = e.step(st, np.zeros((n, 12), dtype=np.float32))
+        before = e._get(_abi.F_STATE)
+        obs_before = st.obs.copy()
+        mask = np.array([1, 0, 0, 1, 0, 1, 0, 0], dtype=np.uint8)
+        keys = make_keys(5, n)
+        kb = _lib.DeviceBuffer(keys.nbytes, e.device)
+        mb = _lib.DeviceBuffer(n, e.device)
+        kb.upload(keys)
+        mb.upload(mask)
+        e.reset_device(kb.ptr.value, mb.ptr.value)
+        e.synchronize()
+        after = e._get(_abi.F_STATE)
+        obs_after = e._get(_abi.F_OBS)
+        kb.free(); mb.free()
+        full = e.reset(keys)
+        for i in range(n):
+            if mask[i]:
+                np.testing.assert_array_equal(after[i], full._record[i])
+                np.testing.assert_array_equal(obs_after[i], full.obs[i])
+            else:
+                np.testing.assert_array_equal(after[i], before[i])
+                np.testing.assert_array_equal(obs_after[i], obs_before[i])
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_single_and_ragged_batches(box_path, n):
+    e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=n)
+    try:
+        keys = make_keys(2, n)
+        st = e.reset(keys if n > 1 else keys[0])
+        oe = O.OracleEnv(e.sys_model.struct, e.config_struct, precision="f32")
+        rs = np.random.RandomState(3)
+        for _ in range(10):
+            a = rs.uniform(-1, 1, size=(n, 12)).astype(np.float32)
+            prev = st
+            st = e.step(prev, a if n > 1 else a[0])
+            rec_prev = prev._record.reshape(n, -1)
+            for i in range(n):
+                o = oe.step(dict(state=G.record_to_oracle_state(rec_prev[i]),
+                                 obs=np.asarray(prev.obs).reshape(n, -1)[i].astype(np.float64)),
+                            a[i].astype(np.float64))
+                rec = st._record.reshape(n, -1)[i]
+                orec = G.oracle_state_to_record(o["state"])
+                np.testing.assert_array_equal(rec[_abi.S_RNG:_abi.S_RNG + 2].view(np.uint32),
+                                              orec[_abi.S_RNG:_abi.S_RNG + 2].view(np.uint32))
+                assert np.abs(np.asarray(st.obs).reshape(n, -1)[i] - o["obs"]).max() <= 5e-3
+                assert abs(np.asarray(st.reward).reshape(n)[i] - o["reward"]) <= 1e-3
+    finally:
+        e.close()
+
+
+def test_max_history_and_latency_lengths(box_path):
+    """observation_history 15 (environment.py:338 comment), 4-long action latency, 3-long IMU latency."""
+    n = 16
+    kw = common.fixture_kwargs(box_path, observation_history=15, latency_distribution=[0.1, 0.2, 0.3, 0.4],
+                               imu_latency_distribution=[0.2, 0.3, 0.5])
+    e = PupperV3Env(**kw, num_envs=n)
+    try:
+        assert e.stride == 98 + 12 * 4 + 6 * 3
+        st = e.reset(make_keys(9, n))
+        assert st.obs.shape == (n, 36 * 15)
+        oe = O.OracleEnv(e.sys_model.struct, e.config_struct, precision="f32")
+        rs = np.random.RandomState(4)
+        for _ in range(20):
+            a = rs.uniform(-1, 1, size=(n, 12)).astype(np.float32)
+            prev = st
+            st = e.step(prev, a)
+            for i in range(n):
+                o = oe.step(dict(state=G.record_to_oracle_state(prev._record[i]), obs=prev.obs[i].astype(np.float64)),
+                            a[i].astype(np.float64))
+                orec = G.oracle_state_to_record(o["state"])
+                assert np.abs(st.obs[i] - o["obs"]).max() <= 5e-3
+                assert abs(st.reward[i] - o["reward"]) <= 1e-3
+                np.testing.assert_allclose(st._record[i, _abi.S_ACT_BUF:], orec[_abi.S_ACT_BUF:], atol=5e-3)
+    finally:
+        e.close()
