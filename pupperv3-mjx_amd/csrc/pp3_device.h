@@ -74,6 +74,7 @@ struct DevModel {
   float pair_k[PP3_MAX_PAIR], pair_b[PP3_MAX_PAIR];
   float pair_margin[PP3_MAX_PAIR];
   float pair_tran[PP3_MAX_PAIR];       // body_invweight0 translational sum
+  int32_t pair_sup[PP3_MAX_PAIR];      // Jacobian column support: leg 0..3 (+base), 4 base only, 5 dense
   float pair_solimp[PP3_MAX_PAIR][5];  // clamped
   // ---- sites ----
   int32_t nsite;
@@ -223,9 +224,15 @@ __device__ __forceinline__ float getimp(const float* si, float pos, float margin
   if (x <= 0.0f) return si[0];
   float y;
   float p = si[4], mid = si[3];
-  if (p == 1.0f) y = x;
-  else if (x <= mid) y = powf(x, p) / powf(mid, p - 1.0f);
-  else y = 1.0f - powf(1.0f - x, p) / powf(1.0f - mid, p - 1.0f);
+  if (p == 1.0f) {
+    y = x;
+  } else if (p == 2.0f) {  // MuJoCo's default power: no powf (4 divergent powf calls cost ~200 VALU)
+    y = (x <= mid) ? x * x / mid : 1.0f - (1.0f - x) * (1.0f - x) / (1.0f - mid);
+  } else if (x <= mid) {
+    y = powf(x, p) / powf(mid, p - 1.0f);
+  } else {
+    y = 1.0f - powf(1.0f - x, p) / powf(1.0f - mid, p - 1.0f);
+  }
   return si[0] + y * (si[1] - si[0]);
 }
 

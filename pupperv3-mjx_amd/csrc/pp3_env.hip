@@ -64,6 +64,7 @@ struct alignas(16) Shared {
   float xpos[NB][3], xquat[NB][4], xaxis[NJ][3];
   float com[4];
   float cinert[NB][10];
+  float crb_base[10], cfrc_base[6];  // root-subtree sums (wave reductions)
   float cdof[NV][6];
   float cvel[NB][6];
   float M[NV][NV + 1];
@@ -72,7 +73,7 @@ struct alignas(16) Shared {
   float qfrc_smooth[NV], qfrc_act[NV], qacc_smooth[NV], Ma[NV], grad[NV], search[NV], dofD[NV];
   // contacts
   int ncon, nhit, nl;
-  int con_pair[NC];
+  int con_pair[NC], con_sup[NC];
   float con_dist[NC], con_mu[NC];
   float con_G[NC][5];
   float Jc[NC][3][NV];
@@ -210,6 +211,20 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int la
     r[5] = A[1][2] - mm * dy * dz;
     r[6] = mm * dx; r[7] = mm * dy; r[8] = mm * dz;
     r[9] = mm;
+  }
+  // composite inertia of the whole tree (body 1's subtree) for the 6 base dofs
+  {
+    float ci[10];
+    const bool body = lane >= 1 && lane < NB;
+#pragma unroll
+    for (int k = 0; k < 10; k++) ci[k] = body ? s.cinert[lane][k] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+      const float t = wave_sum(ci[k]);
+      if (lane == 0) s.crb_base[k] = t;
+    }
+  }
+  if (lane >= 1 && lane < NB) {
   } else if (lane >= 14 && lane < 14 + NV) {
     const int d = lane - 14;
     float* cd = s.cdof[d];
@@ -339,6 +354,7 @@ template <int NC>
 __device__ __forceinline__ void store_contact(Shared<NC>& s, const DevModel& m, int slot, int p, float dist,
                                               const float pos[3], const float nrm[3]) {
   s.con_pair[slot] = p;
+  s.con_sup[slot] = m.pair_sup[p];
   s.con_dist[slot] = dist;
   for (int k = 0; k < 3; k++) s.x.a.con_pos[slot][k] = pos[k];
   make_frame(s.x.a.con_frame[slot], nrm);
@@ -422,18 +438,38 @@ __device__ __forceinline__ void rne_body_forces(Shared<NC>& s, int lane) {
     cross_force(f3, s.cvel[lane], f2);
     for (int k = 0; k < 6; k++) s.x.a.cacc[lane][k] = f1[k] + f3[k];  // cfrc, in place
   }
+  // whole-tree sum of cfrc for the base dofs' bias forces (each lane re-reads its own body)
+  float cf[6];
+  const bool body = lane >= 1 && lane < NB;
+#pragma unroll
+  for (int k = 0; k < 6; k++) cf[k] = body ? s.x.a.cacc[lane][k] : 0.0f;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const float t = wave_sum(cf[k]);
+    if (lane == 0) s.cfrc_base[k] = t;
+  }
 }
 
 // composite inertia of body b's subtree times cdof d (for M), lanes < NV
 template <int NC>
 __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m, int lane) {
   if (lane >= NV) return;
-  const int b = m.dof_body[lane];
-  const int first = b == 1 ? 1 : b, last = b == 1 ? NB - 1 : 2 + 3 * ((b - 2) / 3) + 2;
   float crb[10];
-  for (int k = 0; k < 10; k++) crb[k] = 0;
-  for (int bb = first; bb <= last; bb++)
-    for (int k = 0; k < 10; k++) crb[k] += s.cinert[bb][k];
+  if (lane < 6) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) crb[k] = s.crb_base[k];
+  } else {  // leg link: sum over the (<= 3) links below it in the same leg
+    const int b = m.dof_body[lane], last = 2 + 3 * ((b - 2) / 3) + 2;
+#pragma unroll
+    for (int k = 0; k < 10; k++) crb[k] = s.cinert[b][k];
+#pragma unroll
+    for (int o = 1; o < 3; o++) {
+      const int bb = b + o <= last ? b + o : b;
+      const float w = b + o <= last ? 1.0f : 0.0f;
+#pragma unroll
+      for (int k = 0; k < 10; k++) crb[k] += w * s.cinert[bb][k];
+    }
+  }
   mul_inert_vec(s.x.a.F[lane], crb, s.cdof[lane]);
 }
 
@@ -475,6 +511,16 @@ __device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], 
     x = (lane < k) ? x - col[k] * xk : x;
   }
   return x;  // callers SYNC before s.x is rewritten
+}
+
+// a[j] += w . Jc[.][j] over the columns of support SUP (0..3: base + leg SUP, 4: base, 5: all)
+template <int SUP>
+__device__ __forceinline__ void hess_acc(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    const bool in = SUP == 5 || j < 6 || (SUP < 4 && j >= 6 + 3 * SUP && j < 9 + 3 * SUP);
+    if (in) a[j] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
+  }
 }
 
 // J row r dotted with x (LDS vector)
@@ -606,11 +652,22 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
   PHASE(3);
   // ---- phase 5: qfrc_bias/smooth (subtree sums of body forces), contact edge rows ----
   if (lane < NV) {
-    const int b = m.dof_body[lane];
-    const int first = b == 1 ? 1 : b, last = b == 1 ? NB - 1 : 2 + 3 * ((b - 2) / 3) + 2;
-    float cf[6] = {0, 0, 0, 0, 0, 0};
-    for (int bb = first; bb <= last; bb++)
-      for (int k = 0; k < 6; k++) cf[k] += s.x.a.cacc[bb][k];  // holds cfrc after phase 4
+    float cf[6];
+    if (lane < 6) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) cf[k] = s.cfrc_base[k];
+    } else {  // subtree of a leg link: itself + the (<= 2) links below (cacc holds cfrc now)
+      const int b = m.dof_body[lane], last = 2 + 3 * ((b - 2) / 3) + 2;
+#pragma unroll
+      for (int k = 0; k < 6; k++) cf[k] = s.x.a.cacc[b][k];
+#pragma unroll
+      for (int o = 1; o < 3; o++) {
+        const int bb = b + o <= last ? b + o : b;
+        const float w = b + o <= last ? 1.0f : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) cf[k] += w * s.x.a.cacc[bb][k];
+      }
+    }
     float bias = 0;
     for (int k = 0; k < 6; k++) bias += s.cdof[lane][k] * cf[k];
     s.qfrc_smooth[lane] = -m.dof_damping[lane] * s.qvel[lane] - bias + s.qfrc_act[lane];
@@ -765,8 +822,16 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
         const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
         const float w1 = jn * G[1] + j1 * G[3];
         const float w2 = jn * G[2] + j2 * G[4];
-#pragma unroll
-        for (int j = 0; j < NV; j++) a[j] += w0 * s.Jc[c][0][j] + w1 * s.Jc[c][1][j] + w2 * s.Jc[c][2][j];
+        // J' D J only over the Jacobian's column support (base + one leg for robot-vs-static
+        // contacts): a wave-uniform switch instead of 18 dense columns
+        switch (__builtin_amdgcn_readfirstlane(s.con_sup[c])) {
+          case 0: hess_acc<0>(a, s.Jc[c], w0, w1, w2); break;
+          case 1: hess_acc<1>(a, s.Jc[c], w0, w1, w2); break;
+          case 2: hess_acc<2>(a, s.Jc[c], w0, w1, w2); break;
+          case 3: hess_acc<3>(a, s.Jc[c], w0, w1, w2); break;
+          case 4: hess_acc<4>(a, s.Jc[c], w0, w1, w2); break;
+          default: hess_acc<5>(a, s.Jc[c], w0, w1, w2); break;
+        }
       }
       ldl_rows(a, dinv, lane);
       const float x = ldl_solve(s, a, dinv, s.grad[li], lane);
@@ -1689,6 +1754,18 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
     clamp_solimp(solimp, d->pair_solimp[p]);
     d->pair_margin[p] = (float)(fmax(mm->cgeom_margin[g1], mm->cgeom_margin[g2]) - fmax(mm->cgeom_gap[g1], mm->cgeom_gap[g2]));
     d->pair_tran[p] = (float)(mm->body_invweight0[mm->cgeom_bodyid[g1]][0] + mm->body_invweight0[mm->cgeom_bodyid[g2]][0]);
+    {  // column support of this pair's contact Jacobian (bodies 2..13 = legs of 3 links, 1 = base)
+      auto cls = [](int b) { return b == 0 ? -1 : (b == 1 ? 4 : (b - 2) / 3); };
+      const int c1 = cls(mm->cgeom_bodyid[g1]), c2 = cls(mm->cgeom_bodyid[g2]);
+      int sup;
+      if (c1 < 0) sup = c2;
+      else if (c2 < 0) sup = c1;
+      else if (c1 == c2) sup = c1;
+      else if (c1 == 4) sup = c2;
+      else if (c2 == 4) sup = c1;
+      else sup = 5;
+      d->pair_sup[p] = sup < 0 ? 5 : sup;
+    }
     if (mm->cgeom_margin[g1] != 0 || mm->cgeom_margin[g2] != 0) return set_err(PP3_ERR_MODEL, "nonzero geom margins unsupported");
   }
   d->nsite = mm->nsite;
