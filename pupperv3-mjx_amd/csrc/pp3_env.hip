@@ -28,7 +28,7 @@ constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS tabl
 
 // Phase-local scratch that never lives across a phase boundary it does not own.
 template <int NC>
-union Scratch {
+union alignas(16) Scratch {
   float xipos[NB][3];      // phase 1 (kinematics) -> phase 2 (com_pos)
   struct {                 // phases 3-4
     float F[NV][6];        // crb*cdof -> M entries
@@ -96,6 +96,7 @@ constexpr int NPROF = 16;
 __device__ unsigned long long g_prof[NPROF];
 #define PHASE(k)                                                          \
   do {                                                                    \
+    asm volatile("; PP3PHASE " #k);                                       \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();                     \
     if (lane == 0) { s.prof[k] += t_ - s.prof_t; s.prof_t = t_; }         \
   } while (0)
@@ -488,6 +489,33 @@ __device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int lane) 
     a[k] = (lane > k) ? lik : a[k];
   }
 }
+// Same factorisation with the pivot column broadcast through LDS instead of v_readlane:
+// every lane stores its a[k] (= A'[lane][k] = A'[k][lane]) in col[], then reads col[k..17]
+// back with 16-byte broadcast loads, so each trailing update is one v_fma with VGPR
+// operands (a readlane needs an SGPR hazard s_nop before its consumer).  col = 20 floats,
+// 16-byte aligned, free during the factorisation.
+__device__ __forceinline__ void ldl_rows_lds(float (&a)[NV], float& dinv, int lane, float* col) {
+  const int slot = lane < NV ? lane : NV;  // lanes >= NV carry copies of row NV-1: dummy slot
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    col[slot] = a[k];
+    __syncthreads();
+    float r[20];
+#pragma unroll
+    for (int q = (k & ~3); q < 20; q += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(col + q);
+      r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+    }
+    const float ik = frcp(fmaxf(r[k], MINVAL));
+    dinv = (lane == k) ? ik : dinv;
+    const float lik = a[k] * ik;
+#pragma unroll
+    for (int j = k + 1; j < NV; ++j) a[j] -= lik * r[j];
+    a[k] = (lane > k) ? lik : a[k];
+    __syncthreads();  // col is rewritten by the next pivot
+  }
+}
+
 // solve L D L^T x = b; x = b_i on entry (lane i).  Uses s.x.L for the transposed factor.
 template <int NC>
 __device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int lane) {
@@ -694,7 +722,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
     float a[NV], dinv = 1.0f;
 #pragma unroll
     for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
-    ldl_rows(a, dinv, lane);
+    ldl_rows_lds(a, dinv, lane, &s.x.L[0][0]);
     const float x = ldl_solve(s, a, dinv, s.qfrc_smooth[li], lane);
     if (lane < NV) s.qacc_smooth[lane] = x;
   }
@@ -833,7 +861,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
           default: hess_acc<5>(a, s.Jc[c], w0, w1, w2); break;
         }
       }
-      ldl_rows(a, dinv, lane);
+      ldl_rows_lds(a, dinv, lane, &s.x.L[0][0]);
       const float x = ldl_solve(s, a, dinv, s.grad[li], lane);
       if (lane < NV) s.search[lane] = -x;
     }
