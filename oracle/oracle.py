@@ -43,6 +43,7 @@ def lib(precision: str = "f64") -> C.CDLL:
         L.orc_set_partitionable.argtypes = [C.c_int]
         L.orc_set_ncon_max.argtypes = [C.c_int]
         L.orc_data_size.restype = C.c_size_t
+        L.orc_boundary_take.restype = C.c_int
         _LIBS[name] = L
     return _LIBS[name]
 
@@ -67,7 +68,9 @@ def mj_step(model, qpos, qvel, qacc_ws, ctrl, nsteps=1, dr=None, precision="f64"
     pipe = np.zeros(272, dtype=np.float64) if want_pipe else None
     sites = np.zeros((8, 3), dtype=np.float64)
     d = None if dr is None else np.ascontiguousarray(dr, dtype=np.float64)
+    L.orc_boundary_take()
     L.orc_mj_step(C.byref(model), _p(d), ncon_max, _p(q), _p(v), _p(w), _p(c), nsteps, _p(pipe), _p(sites))
+    mj_step.last_boundary = L.orc_boundary_take()
     return q, v, w, pipe, sites
 
 
@@ -116,9 +119,13 @@ class OracleEnv:
         met = np.zeros(19)
         pipe = np.zeros(272)
         a = np.ascontiguousarray(action, dtype=np.float64)
+        self.L.orc_boundary_take()
         self.L.orc_env_step(C.byref(self.model), C.byref(self.cfg), _p(self.dr), _p(st), _p(obs), _p(a),
                             _p(rew), _p(done), _p(met), _p(pipe))
-        return dict(state=st, obs=obs, reward=rew[0], done=done[0], metrics=met, pipe=pipe)
+        # rows decided within rounding of a constraint-state switch during this step (see
+        # pp3_oracle.c BOUNDARY_REL): there an fp32 kernel may legitimately take the other branch
+        nb = self.L.orc_boundary_take()
+        return dict(state=st, obs=obs, reward=rew[0], done=done[0], metrics=met, pipe=pipe, boundary=nb)
 
 
 def rollout(model, cfg, states, obs, actions, nsteps, nthreads=0, precision="f64"):

@@ -95,6 +95,9 @@ void orc_threefry2x32(uint32_t k0, uint32_t k1, uint32_t x0, uint32_t x1, uint32
 typedef struct { uint32_t k[2]; } key_t2;
 
 static int g_partitionable = 1;
+static double g_dbg[512];
+static int g_boundary = 0;  /* near-switch constraint rows seen since the last orc_boundary_take() */
+#define BOUNDARY_REL ((real)1e-4)  /* last Newton iteration's intermediates (debugging aid) */
 static int g_ncon_max = 0; /* contact cap shared with the HIP kernel: 0 = auto (8 flat, 16 with boxes) */
 
 /* jax.random.split(key, n)[i] */
@@ -1030,6 +1033,7 @@ static void solve_newton(const Model* m, Data* d) {
   mulM(d, Ma, d->qacc_warmstart);
   for (int i = 0; i < NV; i++) cost_ws += (real)0.5 * (Ma[i] - d->qfrc_smooth[i]) * (d->qacc_warmstart[i] - d->qacc_smooth[i]);
   real cost_sm = constraint_update(d, jar_s, 0);
+  if (RFABS(cost_ws - cost_sm) < BOUNDARY_REL * (RFABS(cost_ws) + RFABS(cost_sm))) g_boundary++;
   if (cost_ws > cost_sm) memcpy(qacc, d->qacc_smooth, sizeof(qacc));
   else memcpy(qacc, d->qacc_warmstart, sizeof(qacc));
 
@@ -1044,6 +1048,18 @@ static void solve_newton(const Model* m, Data* d) {
       jar[r] = s - d->efc_aref[r];
     }
     real cost = constraint_update(d, jar, 1);
+    /* fp32 sensitivity flag: a row whose constraint state (satisfied / quadratic / linear) is
+     * decided within rounding of its switch point makes the Newton Hessian, and so this
+     * one-iteration solve, discontinuous in the input; count such rows for the parity tests */
+    for (int r = 0; r < nefc; r++) {
+      const real x = jar[r], sc = BOUNDARY_REL * (1 + RFABS(d->efc_aref[r]));
+      if (d->efc_type[r] == CN_FRICTION) {
+        const real rf = d->efc_R[r] * d->efc_floss[r];
+        if (RFABS(x - rf) < sc || RFABS(x + rf) < sc) g_boundary++;
+      } else if (RFABS(x) < sc) {
+        g_boundary++;
+      }
+    }
     real gauss = 0;
     for (int i = 0; i < NV; i++) gauss += (real)0.5 * (Ma[i] - d->qfrc_smooth[i]) * (qacc[i] - d->qacc_smooth[i]);
     cost += gauss;
@@ -1063,6 +1079,13 @@ static void solve_newton(const Model* m, Data* d) {
         if (ji == 0) continue;
         for (int j = 0; j < NV; j++) H[i][j] += ji * d->efc_J[r][j];
       }
+    }
+    for (int i = 0; i < NV; i++)
+      for (int j = 0; j < NV; j++) g_dbg[64 + NV * i + j] = (double)H[i][j];
+    for (int r = 12; r < nefc && r < 20; r++) {
+      g_dbg[400 + r - 12] = d->efc_state[r] == ST_QUADRATIC ? (double)d->efc_D[r] : 0.0;
+      g_dbg[430 + r - 12] = (double)jar[r];
+      g_dbg[440 + r - 12] = (double)d->efc_force[r];
     }
     chol_factor(H);
     chol_solve(H, search, grad);
@@ -1090,6 +1113,11 @@ static void solve_newton(const Model* m, Data* d) {
     }
     real gtol = m->tolerance * m->ls_tolerance * snorm / scale;
     real alpha = line_search(&c, gtol, m->ls_iterations);
+    /* debug record of the last Newton iteration (orc_debug_read) */
+    for (int i = 0; i < NV; i++) { g_dbg[i] = (double)qacc[i]; g_dbg[18 + i] = (double)grad[i]; g_dbg[36 + i] = (double)search[i]; }
+    g_dbg[54] = (double)c.quadG[0]; g_dbg[55] = (double)c.quadG[1]; g_dbg[56] = (double)c.quadG[2];
+    g_dbg[57] = (double)snorm; g_dbg[58] = (double)gtol; g_dbg[59] = (double)alpha; g_dbg[60] = (double)c.evals;
+    g_dbg[61] = (double)cost_ws; g_dbg[62] = (double)cost_sm; g_dbg[63] = (double)nefc;
     d->ls_evals += c.evals;
     if (alpha == 0) break;
     for (int i = 0; i < NV; i++) qacc[i] += alpha * search[i];
@@ -1629,6 +1657,8 @@ int orc_env_rollout(const pp3_model_t* mm, const pp3_env_config_t* cfg, int n, i
 }
 
 void orc_set_ncon_max(int n) { g_ncon_max = n; }
+void orc_debug_read(double* out) { memcpy(out, g_dbg, sizeof(g_dbg)); }
+int orc_boundary_take(void) { const int n = g_boundary; g_boundary = 0; return n; }
 
 /* RNG test hooks */
 void orc_set_partitionable(int p) { g_partitionable = p; }

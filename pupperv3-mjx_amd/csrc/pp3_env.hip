@@ -1,14 +1,19 @@
 // pp3_env.hip -- MI355X (gfx950) kernels for the Pupper-v3 environment hot path.
 //
-// One wavefront (64 lanes) per environment, one environment per workgroup.  The whole
-// env step of PupperV3Env.step (environment.py:348-483) runs in ONE launch: RNG/kick/
-// latency prologue, n_frames (=5) MuJoCo-semantics physics substeps (kinematics, CRB mass
-// matrix, collision, pyramidal contact + frictionloss + limit constraints, RNE, Newton
-// solve with exact line search, Euler), then the observation/reward/termination epilogue.
-// Per-env state lives in LDS for the whole launch (<= 10 KB per env so 16 envs = 16 waves
-// are resident per CU); HBM sees one read and one write of the env's state record per env
-// step.  Small dense linear algebra (18x18 LDL^T) runs in registers, one matrix row per
-// lane, with v_readlane broadcasts.
+// TWO environments per 64-lane wavefront: lanes 0..31 own env 2b, lanes 32..63 own env
+// 2b+1 (workgroup b = one wave).  The whole env step of PupperV3Env.step
+// (environment.py:348-483) runs in ONE launch: RNG/kick/latency prologue, n_frames (=5)
+// MuJoCo-semantics physics substeps (kinematics, CRB mass matrix, collision, pyramidal
+// contact + frictionloss + limit constraints, RNE, Newton solve with exact line search,
+// Euler), then the observation/reward/termination epilogue.
+//
+// Why two per wave: the kernel is VALU-issue bound (rocprofv3: SQ_WAVE_CYCLES ~= 4 waves x
+// SQ_INSTS_VALU x 4 cycles) and almost every phase needs <= 32 lanes per env (13 bodies,
+// 18 dofs, 32 candidate pairs, <= 3 constraint rows per lane), so packing two envs into one
+// wave halves the VALU instructions per env.  Per-env state lives in LDS for the whole
+// launch (~10 KB per env, 8 waves = 16 envs per CU); HBM sees one read and one write of
+// each env's state record per env step.  18x18 LDL^T runs one matrix row per lane with the
+// pivot column broadcast through LDS; half-wave reductions run on the DPP network.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -22,9 +27,11 @@
 
 namespace pp3 {
 
-constexpr int HMAX = 16;  // observation_history limit
-constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + WAVE - 1) / WAVE;
+constexpr int HW = 32;      // lanes per environment (half wave)
+constexpr int HMAX = 16;    // observation_history limit
+constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + HW - 1) / HW;
 constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
+constexpr int NHIT = 64;        // contact-overflow ranking window (hits kept for ranking)
 
 // Phase-local scratch that never lives across a phase boundary it does not own.
 template <int NC>
@@ -33,12 +40,12 @@ union alignas(16) Scratch {
   struct {                 // phases 3-4
     float F[NV][6];        // crb*cdof -> M entries
     float cacc[NB][6];     // rne chain -> body forces (overwritten in place by cfrc)
-    float hit_dist[WAVE];  // collision overflow ranking
-    int hit_pair[WAVE];
+    float hit_dist[NHIT];  // collision overflow ranking
+    int hit_pair[NHIT];
     float con_pos[NC][3];  // collision -> contact Jacobians
     float con_frame[NC][9];
   } a;
-  float L[NV][NV + 1];     // LDL factor rows (transposed reads), phases 6-8
+  float L[NV][NV + 1];     // LDL pivot column (row 0) / transposed factor, phases 5-7
   struct {                 // env prologue / epilogue
     float u[40];
     float o[PP3_OBS_DIM];
@@ -64,7 +71,7 @@ struct alignas(16) Shared {
   float xpos[NB][3], xquat[NB][4], xaxis[NJ][3];
   float com[4];
   float cinert[NB][10];
-  float crb_base[10], cfrc_base[6];  // root-subtree sums (wave reductions)
+  float crb_base[10], cfrc_base[6];  // root-subtree sums (half-wave reductions)
   float cdof[NV][6];
   float cvel[NB][6];
   float M[NV][NV + 1];
@@ -98,7 +105,7 @@ __device__ unsigned long long g_prof[NPROF];
   do {                                                                    \
     asm volatile("; PP3PHASE " #k);                                       \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();                     \
-    if (lane == 0) { s.prof[k] += t_ - s.prof_t; s.prof_t = t_; }         \
+    if (l == 0) { s.prof[k] += t_ - s.prof_t; s.prof_t = t_; }            \
   } while (0)
 #else
 #define PHASE(k) do { } while (0)
@@ -106,36 +113,72 @@ __device__ unsigned long long g_prof[NPROF];
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+#ifdef PP3_DEBUG
+__device__ float g_dbg[512];  // last Newton iteration of env 0 (debug build only)
+#endif
+
+// ---------------------------- half-wave primitives ----------------------------
+// value of lane k of this lane's half (k compile-time or wave-uniform)
+__device__ __forceinline__ float hb(float v, int k, int h) {
+  const float a = rlane(v, k), b = rlane(v, k + HW);
+  return h ? b : a;
+}
+__device__ __forceinline__ uint32_t hbu(uint32_t v, int k, int h) {
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, k + HW);
+  return h ? b : a;
+}
+__device__ __forceinline__ Key hkey(Key k, int l, int h) { return Key{hbu(k.a, l, h), hbu(k.b, l, h)}; }
+// sum over the 32 lanes of this lane's half: DPP butterflies inside each 16-lane row,
+// row_bcast:15 folds row 0 into row 1 (and row 2 into row 3); lanes 31 / 63 hold the totals
+__device__ __forceinline__ float hsum(float v, int h) {
+  v += dpp_f<0xB1, 0xF>(v, 0.0f);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xF>(v, 0.0f);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xF>(v, 0.0f);  // row_half_mirror
+  v += dpp_f<0x140, 0xF>(v, 0.0f);  // row_mirror
+  v += dpp_f<0x142, 0xA>(v, 0.0f);  // row_bcast:15 -> rows 1, 3
+  return hb(v, HW - 1, h);
+}
+// this half's bits of a ballot
+__device__ __forceinline__ uint32_t hballot(bool p, int h) {
+  const uint64_t m = __ballot(p);
+  return h ? (uint32_t)(m >> 32) : (uint32_t)m;
+}
+// max over both halves of a half-uniform int (wave-uniform loop bound)
+__device__ __forceinline__ int wmax2(int v) {
+  const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, HW);
+  return a > b ? a : b;
+}
+
 // ------------------------------------------------------------------------------------
 // Phase 1: forward kinematics (mj_kinematics).  12 lanes build the local link rotations
 // (body_quat * joint rotation) in parallel, then lanes 0..3 compose base -> leg chain.
 // Hinge anchors coincide with body origins (jnt_pos = 0, checked at pp3_create).
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int lane) {
-  // local quaternion of link (leg l, level k) in lane 4k + l (lanes 0..11)
+__device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l) {
   float lq[4] = {1, 0, 0, 0};
-  if (lane < 12) {
-    const int l = lane & 3, k = lane >> 2;
-    const int b = 2 + 3 * l + k, j = 1 + 3 * l + k, qa = 7 + 3 * l + k;
+  if (l < 12) {
+    const int g = l & 3, k = l >> 2;
+    const int b = 2 + 3 * g + k, j = 1 + 3 * g + k, qa = 7 + 3 * g + k;
     float qloc[4];
     axisangle2quat(qloc, m.jnt_axis[j], s.qpos[qa] - m.qpos0[qa]);
     mulquat(lq, m.body_quat[b], qloc);
   }
-  // broadcast the 3 levels of this lane's leg (lanes 0..3 consume)
+  // the 3 levels of this lane's leg (lanes 0..3 consume); width-32 shuffles stay in the half
   float lq1[4], lq2[4];
 #pragma unroll
   for (int c = 0; c < 4; c++) {
-    lq1[c] = __shfl(lq[c], (lane & 3) + 4, WAVE);
-    lq2[c] = __shfl(lq[c], (lane & 3) + 8, WAVE);
+    lq1[c] = __shfl(lq[c], (l & 3) + 4, HW);
+    lq2[c] = __shfl(lq[c], (l & 3) + 8, HW);
   }
-  if (lane < 4) {
+  if (l < 4) {
     float pq[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
     normalize4(pq);
     float pp[3] = {s.qpos[0], s.qpos[1], s.qpos[2]};
     float pR[9];
     quat2mat(pq, pR);
-    if (lane == 0) {
+    if (l == 0) {
       float off[3];
       matvec(off, pR, s.ipos[1]);
       for (int c = 0; c < 3; c++) {
@@ -147,7 +190,7 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
     }
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      const int b = 2 + 3 * lane + k, j = 1 + 3 * lane + k;
+      const int b = 2 + 3 * l + k, j = 1 + 3 * l + k;
       const float* lqk = k == 0 ? lq : (k == 1 ? lq1 : lq2);
       float xp[3], xq[4], off[3], R[9], ax[3];
       matvec(off, pR, m.body_pos[b]);
@@ -171,26 +214,31 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
 
 // ------------------------------------------------------------------------------------
 // Phase 2: subtree com, cinert (mju_inertCom), cdof, robot geom and foot-site positions.
+// lanes 1..13 bodies, 14..31 dofs; then lanes 0..7 geoms, 16..19 feet.
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int lane) {
+__device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h) {
+  const bool body = l >= 1 && l < NB;
   float mb = 0, mx = 0, my = 0, mz = 0;
-  if (lane >= 1 && lane < NB) {
-    mb = s.mass[lane];
-    mx = mb * s.x.xipos[lane][0];
-    my = mb * s.x.xipos[lane][1];
-    mz = mb * s.x.xipos[lane][2];
+  if (body) {
+    mb = s.mass[l];
+    mx = mb * s.x.xipos[l][0];
+    my = mb * s.x.xipos[l][1];
+    mz = mb * s.x.xipos[l][2];
   }
-  mb = wave_sum(mb);
-  mx = wave_sum(mx);
-  my = wave_sum(my);
-  mz = wave_sum(mz);
+  mb = hsum(mb, h);
+  mx = hsum(mx, h);
+  my = hsum(my, h);
+  mz = hsum(mz, h);
   float com[3];
   if (mb > MINVAL) { const float im = 1.0f / mb; com[0] = mx * im; com[1] = my * im; com[2] = mz * im; }
   else { com[0] = s.x.xipos[1][0]; com[1] = s.x.xipos[1][1]; com[2] = s.x.xipos[1][2]; }
-  if (lane == 0) { s.com[0] = com[0]; s.com[1] = com[1]; s.com[2] = com[2]; }
-  if (lane >= 1 && lane < NB) {
-    const int b = lane;
+  if (l == 0) { s.com[0] = com[0]; s.com[1] = com[1]; s.com[2] = com[2]; }
+  float ci[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) ci[k] = 0.0f;
+  if (body) {
+    const int b = l;
     float iq[4], R[9];
     mulquat(iq, s.xquat[b], m.body_iquat[b]);
     quat2mat(iq, R);
@@ -203,31 +251,18 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int la
         A[i][j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
     const float mm = s.mass[b];
     const float dx = s.x.xipos[b][0] - com[0], dy = s.x.xipos[b][1] - com[1], dz = s.x.xipos[b][2] - com[2];
-    float* r = s.cinert[b];
-    r[0] = A[0][0] + mm * (dy * dy + dz * dz);
-    r[1] = A[1][1] + mm * (dx * dx + dz * dz);
-    r[2] = A[2][2] + mm * (dx * dx + dy * dy);
-    r[3] = A[0][1] - mm * dx * dy;
-    r[4] = A[0][2] - mm * dx * dz;
-    r[5] = A[1][2] - mm * dy * dz;
-    r[6] = mm * dx; r[7] = mm * dy; r[8] = mm * dz;
-    r[9] = mm;
-  }
-  // composite inertia of the whole tree (body 1's subtree) for the 6 base dofs
-  {
-    float ci[10];
-    const bool body = lane >= 1 && lane < NB;
+    ci[0] = A[0][0] + mm * (dy * dy + dz * dz);
+    ci[1] = A[1][1] + mm * (dx * dx + dz * dz);
+    ci[2] = A[2][2] + mm * (dx * dx + dy * dy);
+    ci[3] = A[0][1] - mm * dx * dy;
+    ci[4] = A[0][2] - mm * dx * dz;
+    ci[5] = A[1][2] - mm * dy * dz;
+    ci[6] = mm * dx; ci[7] = mm * dy; ci[8] = mm * dz;
+    ci[9] = mm;
 #pragma unroll
-    for (int k = 0; k < 10; k++) ci[k] = body ? s.cinert[lane][k] : 0.0f;
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-      const float t = wave_sum(ci[k]);
-      if (lane == 0) s.crb_base[k] = t;
-    }
-  }
-  if (lane >= 1 && lane < NB) {
-  } else if (lane >= 14 && lane < 14 + NV) {
-    const int d = lane - 14;
+    for (int k = 0; k < 10; k++) s.cinert[b][k] = ci[k];
+  } else if (l >= 14) {
+    const int d = l - 14;
     float* cd = s.cdof[d];
     if (d < 3) {
       for (int k = 0; k < 6; k++) cd[k] = 0;
@@ -249,31 +284,38 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int la
       cross3(c, ax, off);
       for (int k = 0; k < 3; k++) { cd[k] = ax[k]; cd[3 + k] = c[k]; }
     }
-  } else if (lane >= 32 && lane < 32 + m.nrobot_geom) {
-    const int g = m.robot_geom[lane - 32], b = m.cg_body[g];
+  }
+  // composite inertia of the whole tree (body 1's subtree) for the 6 base dofs
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    const float t = hsum(ci[k], h);
+    if (l == 0) s.crb_base[k] = t;
+  }
+  // world positions of the robot collision spheres (lanes 0..7) and foot sites (16..19)
+  const bool geom = l < m.nrobot_geom, foot = l >= 16 && l < 20;
+  if (geom || foot) {
+    int b;
+    const float* lp;
+    if (geom) { const int g = m.robot_geom[l]; b = m.cg_body[g]; lp = m.cg_pos[g]; }
+    else { const int si = m.feet_site[l - 16]; b = m.site_body[si]; lp = m.site_pos[si]; }
     float R[9], off[3];
     quat2mat(s.xquat[b], R);
-    matvec(off, R, m.cg_pos[g]);
-    for (int k = 0; k < 3; k++) s.gxpos[lane - 32][k] = s.xpos[b][k] + off[k];
-  } else if (lane >= 48 && lane < 52) {
-    const int f = lane - 48, si = m.feet_site[f], b = m.site_body[si];
-    float R[9], off[3];
-    quat2mat(s.xquat[b], R);
-    matvec(off, R, m.site_pos[si]);
-    for (int k = 0; k < 3; k++) s.foot_xpos[f][k] = s.xpos[b][k] + off[k];
+    matvec(off, R, lp);
+    float* dst = geom ? s.gxpos[l] : s.foot_xpos[l - 16];
+    for (int k = 0; k < 3; k++) dst[k] = s.xpos[b][k] + off[k];
   }
 }
 
 __device__ __forceinline__ void make_frame(float f[9], const float nin[3]) {
   float a[3] = {nin[0], nin[1], nin[2]};
   float n = sqrtf(dot3(a, a));
-  if (n < MINVAL) { a[0] = 1; a[1] = 0; a[2] = 0; } else { a[0] /= n; a[1] /= n; a[2] /= n; }
+  if (n < MINVAL) { a[0] = 1; a[1] = 0; a[2] = 0; } else { const float in = 1.0f / n; a[0] *= in; a[1] *= in; a[2] *= in; }
   float y[3] = {0, 0, 0};
   if (a[1] < 0.5f && a[1] > -0.5f) y[1] = 1; else y[2] = 1;
   float ad = dot3(a, y);
   for (int k = 0; k < 3; k++) y[k] -= a[k] * ad;
   float yn = sqrtf(dot3(y, y));
-  if (yn < MINVAL) { y[0] = 1; y[1] = 0; y[2] = 0; } else { y[0] /= yn; y[1] /= yn; y[2] /= yn; }
+  if (yn < MINVAL) { y[0] = 1; y[1] = 0; y[2] = 0; } else { const float in = 1.0f / yn; y[0] *= in; y[1] *= in; y[2] *= in; }
   float z[3];
   cross3(z, a, y);
   for (int k = 0; k < 3; k++) { f[k] = a[k]; f[3 + k] = y[k]; f[6 + k] = z[k]; }
@@ -315,15 +357,15 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, i
   }
   if (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_BOX) {
     const float* R2 = m.cg_wmat[g2];
-    const float* h = m.cg_size[g2];
+    const float* hh = m.cg_size[g2];
     float r = m.cg_size[g1][0];
     float rel[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]}, dl[3], cl[3];
     for (int k = 0; k < 3; k++) dl[k] = R2[k] * rel[0] + R2[3 + k] * rel[1] + R2[6 + k] * rel[2];
     bool inside = true;
     for (int k = 0; k < 3; k++) {
       cl[k] = dl[k];
-      if (cl[k] > h[k]) { cl[k] = h[k]; inside = false; }
-      if (cl[k] < -h[k]) { cl[k] = -h[k]; inside = false; }
+      if (cl[k] > hh[k]) { cl[k] = hh[k]; inside = false; }
+      if (cl[k] < -hh[k]) { cl[k] = -hh[k]; inside = false; }
     }
     float nl[3], dd;
     if (!inside) {
@@ -332,9 +374,9 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, i
       dd = len - r;
       if (dd > margin) return false;
       if (len < MINVAL) { nl[0] = 0; nl[1] = 0; nl[2] = -1; }
-      else { for (int k = 0; k < 3; k++) nl[k] = v[k] / len; }
+      else { const float il = 1.0f / len; for (int k = 0; k < 3; k++) nl[k] = v[k] * il; }
     } else {
-      const float t0 = h[0] - fabsf(dl[0]), t1b = h[1] - fabsf(dl[1]), t2b = h[2] - fabsf(dl[2]);
+      const float t0 = hh[0] - fabsf(dl[0]), t1b = hh[1] - fabsf(dl[1]), t2b = hh[2] - fabsf(dl[2]);
       const int ax = (t1b < t0 && t1b <= t2b) ? 1 : (t2b < t0 && t2b < t1b) ? 2 : 0;
       const float best = ax == 0 ? t0 : (ax == 1 ? t1b : t2b);
       const float sg = (ax == 0 ? dl[0] : (ax == 1 ? dl[1] : dl[2])) >= 0 ? -1.0f : 1.0f;
@@ -365,39 +407,59 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const DevModel& m, 
 // Phase 3a: collision (mj_collision), contacts compacted in pair order; when more than
 // NC pairs penetrate, the NC deepest are kept (same rule as the oracle).
 template <int NC>
-__device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int lane) {
+__device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int l, int h) {
   int nhit = 0;
-  for (int base = 0; base < m.npair; base += WAVE) {
-    const int p = base + lane;
+  for (int base = 0; base < m.npair; base += HW) {
+    const int p = base + l;
     float dist = 0, pos[3], nrm[3];
-    bool hit = (p < m.npair) && narrow(s, m, p, dist, pos, nrm);
-    const uint64_t mask = __ballot(hit);
-    const int slot = nhit + __popcll(mask & ((1ull << lane) - 1ull));
+    const bool hit = (p < m.npair) && narrow(s, m, p, dist, pos, nrm);
+    const uint32_t mask = hballot(hit, h);
+    const int slot = nhit + __popc(mask & ((1u << l) - 1u));
     if (hit) {
       if (slot < NC) store_contact(s, m, slot, p, dist, pos, nrm);
-      if (slot < WAVE) { s.x.a.hit_dist[slot] = dist; s.x.a.hit_pair[slot] = p; }
+      if (slot < NHIT) { s.x.a.hit_dist[slot] = dist; s.x.a.hit_pair[slot] = p; }
     }
-    nhit += __popcll(mask);
+    nhit += __popc(mask);
   }
-  if (lane == 0) { s.nhit = nhit; s.ncon = nhit < NC ? nhit : NC; }
-  if (nhit > NC) {  // rare: keep the NC deepest among the first WAVE hits, in pair order
+  if (l == 0) { s.nhit = nhit; s.ncon = nhit < NC ? nhit : NC; }
+  const bool ovf = nhit > NC;
+  if (__ballot(ovf)) {  // rare: keep the NC deepest among the first NHIT hits, in pair order
     SYNC();
-    const int nh = nhit < WAVE ? nhit : WAVE;
-    const float myd = lane < nh ? s.x.a.hit_dist[lane] : 0.0f;
-    int rank = 0;
-    for (int c = 0; c < nh; c++) {
-      const float dc = s.x.a.hit_dist[c];
-      rank += (dc < myd || (dc == myd && c < lane)) ? 1 : 0;
+    const int nh = nhit < NHIT ? nhit : NHIT;
+    int keep_p[NHIT / HW];
+    bool keep[NHIT / HW];
+    int rank[NHIT / HW];
+#pragma unroll
+    for (int t = 0; t < NHIT / HW; t++) {
+      const int i = l + HW * t;
+      const float myd = i < nh ? s.x.a.hit_dist[i] : 0.0f;
+      int r = 0;
+      for (int c = 0; c < nh; c++) {
+        const float dc = s.x.a.hit_dist[c];
+        r += (dc < myd || (dc == myd && c < i)) ? 1 : 0;
+      }
+      rank[t] = r;
+      keep[t] = ovf && i < nh && r < NC;
+      keep_p[t] = i < nh ? s.x.a.hit_pair[i] : 0;
     }
-    const bool keep = lane < nh && rank < NC;
-    const uint64_t km = __ballot(keep);
-    const int slot = __popcll(km & ((1ull << lane) - 1ull));
-    const int p = lane < nh ? s.x.a.hit_pair[lane] : 0;
+    // slot = number of kept hits with a smaller hit index
+    int before = 0;
+    int slot[NHIT / HW];
+#pragma unroll
+    for (int t = 0; t < NHIT / HW; t++) {
+      const uint32_t km = hballot(keep[t], h);
+      slot[t] = before + __popc(km & ((1u << l) - 1u));
+      before += __popc(km);
+    }
+    (void)rank;
     SYNC();
-    if (keep) {
-      float dist, pos[3], nrm[3];
-      narrow(s, m, p, dist, pos, nrm);
-      store_contact(s, m, slot, p, dist, pos, nrm);
+#pragma unroll
+    for (int t = 0; t < NHIT / HW; t++) {
+      if (keep[t]) {
+        float dist, pos[3], nrm[3];
+        narrow(s, m, keep_p[t], dist, pos, nrm);
+        store_contact(s, m, slot[t], keep_p[t], dist, pos, nrm);
+      }
     }
   }
 }
@@ -405,8 +467,8 @@ __device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int 
 // RNE velocity/acceleration chain (mj_comVel + forward half of mj_rne): lanes 0..3 each
 // walk base -> leg l writing cvel and cacc of its links (lane 0 also the base).
 template <int NC>
-__device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int lane) {
-  if (lane >= 4) return;
+__device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int l) {
+  if (l >= 4) return;
   float cv[6] = {0, 0, 0, 0, 0, 0}, ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
   for (int d = 0; d < 3; d++)
     for (int k = 0; k < 6; k++) cv[k] += s.cdof[d][k] * s.qvel[d];
@@ -417,11 +479,11 @@ __device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int 
   }
   for (int d = 0; d < 3; d++)
     for (int k = 0; k < 6; k++) cv[k] += s.cdof[3 + d][k] * s.qvel[3 + d];
-  if (lane == 0)
+  if (l == 0)
     for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv[k]; s.x.a.cacc[1][k] = ca[k]; }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const int b = 2 + 3 * lane + k, d = 6 + 3 * lane + k;
+    const int b = 2 + 3 * l + k, d = 6 + 3 * l + k;
     cross_motion(cdd, cv, s.cdof[d]);
     const float qd = s.qvel[d];
     for (int c = 0; c < 6; c++) { cv[c] += s.cdof[d][c] * qd; ca[c] += cdd[c] * qd; }
@@ -429,38 +491,35 @@ __device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int 
   }
 }
 
-// body forces cinert*cacc + cvel x* (cinert*cvel), lanes 1..13 (one body each)
+// body forces cinert*cacc + cvel x* (cinert*cvel), lanes 1..13 (one body each), plus the
+// whole-tree sum of cfrc for the base dofs' bias forces
 template <int NC>
-__device__ __forceinline__ void rne_body_forces(Shared<NC>& s, int lane) {
-  if (lane >= 1 && lane < NB) {
+__device__ __forceinline__ void rne_body_forces(Shared<NC>& s, int l, int h) {
+  float cf[6] = {0, 0, 0, 0, 0, 0};
+  if (l >= 1 && l < NB) {
     float f1[6], f2[6], f3[6];
-    mul_inert_vec(f1, s.cinert[lane], s.x.a.cacc[lane]);
-    mul_inert_vec(f2, s.cinert[lane], s.cvel[lane]);
-    cross_force(f3, s.cvel[lane], f2);
-    for (int k = 0; k < 6; k++) s.x.a.cacc[lane][k] = f1[k] + f3[k];  // cfrc, in place
+    mul_inert_vec(f1, s.cinert[l], s.x.a.cacc[l]);
+    mul_inert_vec(f2, s.cinert[l], s.cvel[l]);
+    cross_force(f3, s.cvel[l], f2);
+    for (int k = 0; k < 6; k++) { cf[k] = f1[k] + f3[k]; s.x.a.cacc[l][k] = cf[k]; }  // cfrc, in place
   }
-  // whole-tree sum of cfrc for the base dofs' bias forces (each lane re-reads its own body)
-  float cf[6];
-  const bool body = lane >= 1 && lane < NB;
-#pragma unroll
-  for (int k = 0; k < 6; k++) cf[k] = body ? s.x.a.cacc[lane][k] : 0.0f;
 #pragma unroll
   for (int k = 0; k < 6; k++) {
-    const float t = wave_sum(cf[k]);
-    if (lane == 0) s.cfrc_base[k] = t;
+    const float t = hsum(cf[k], h);
+    if (l == 0) s.cfrc_base[k] = t;
   }
 }
 
 // composite inertia of body b's subtree times cdof d (for M), lanes < NV
 template <int NC>
-__device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m, int lane) {
-  if (lane >= NV) return;
+__device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m, int l) {
+  if (l >= NV) return;
   float crb[10];
-  if (lane < 6) {
+  if (l < 6) {
 #pragma unroll
     for (int k = 0; k < 10; k++) crb[k] = s.crb_base[k];
   } else {  // leg link: sum over the (<= 3) links below it in the same leg
-    const int b = m.dof_body[lane], last = 2 + 3 * ((b - 2) / 3) + 2;
+    const int b = m.dof_body[l], last = 2 + 3 * ((b - 2) / 3) + 2;
 #pragma unroll
     for (int k = 0; k < 10; k++) crb[k] = s.cinert[b][k];
 #pragma unroll
@@ -471,31 +530,18 @@ __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m,
       for (int k = 0; k < 10; k++) crb[k] += w * s.cinert[bb][k];
     }
   }
-  mul_inert_vec(s.x.a.F[lane], crb, s.cdof[lane]);
+  mul_inert_vec(s.x.a.F[l], crb, s.cdof[l]);
 }
 
 // ------------------------------------------------------------------------------------
-// register LDL^T: lane i (< NV) holds row i; returns L_ik (k<i) in a[k], 1/D_i in dinv
+// LDL^T in registers: lane i (< NV) of each half holds row i; returns L_ik (k<i) in a[k],
+// 1/D_i in dinv.  The pivot column is broadcast through LDS: every lane stores its a[k]
+// (= A'[lane][k] = A'[k][lane]) in col[], then reads col[k..17] back with 16-byte broadcast
+// loads, so each trailing update is one v_fma with VGPR operands.  col = 20 floats, 16-byte
+// aligned, owned by this half.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int lane) {
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const float dk = fmaxf(rlane(a[k], k), MINVAL);
-    const float ik = frcp(dk);
-    dinv = (lane == k) ? ik : dinv;
-    const float lik = a[k] * ik;
-#pragma unroll
-    for (int j = k + 1; j < NV; ++j) a[j] -= lik * rlane(a[k], j);
-    a[k] = (lane > k) ? lik : a[k];
-  }
-}
-// Same factorisation with the pivot column broadcast through LDS instead of v_readlane:
-// every lane stores its a[k] (= A'[lane][k] = A'[k][lane]) in col[], then reads col[k..17]
-// back with 16-byte broadcast loads, so each trailing update is one v_fma with VGPR
-// operands (a readlane needs an SGPR hazard s_nop before its consumer).  col = 20 floats,
-// 16-byte aligned, free during the factorisation.
-__device__ __forceinline__ void ldl_rows_lds(float (&a)[NV], float& dinv, int lane, float* col) {
-  const int slot = lane < NV ? lane : NV;  // lanes >= NV carry copies of row NV-1: dummy slot
+__device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int l, float* col) {
+  const int slot = l < NV ? l : NV;  // lanes >= NV carry copies of row NV-1: dummy slot
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     col[slot] = a[k];
@@ -507,26 +553,25 @@ __device__ __forceinline__ void ldl_rows_lds(float (&a)[NV], float& dinv, int la
       r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
     }
     const float ik = frcp(fmaxf(r[k], MINVAL));
-    dinv = (lane == k) ? ik : dinv;
+    dinv = (l == k) ? ik : dinv;
     const float lik = a[k] * ik;
 #pragma unroll
     for (int j = k + 1; j < NV; ++j) a[j] -= lik * r[j];
-    a[k] = (lane > k) ? lik : a[k];
+    a[k] = (l > k) ? lik : a[k];
     __syncthreads();  // col is rewritten by the next pivot
   }
 }
-
 // solve L D L^T x = b; x = b_i on entry (lane i).  Uses s.x.L for the transposed factor.
 template <int NC>
-__device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int lane) {
-  const int li = lane < NV ? lane : NV - 1;
+__device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int l, int h) {
+  const int li = l < NV ? l : NV - 1;
 #pragma unroll
   for (int k = 0; k < NV; ++k)
-    if (k < lane && lane < NV) s.x.L[lane][k] = a[k];
+    if (k < l && l < NV) s.x.L[l][k] = a[k];
 #pragma unroll
   for (int k = 0; k < NV - 1; ++k) {
-    const float yk = rlane(x, k);
-    x = (lane > k) ? x - a[k] * yk : x;
+    const float yk = hb(x, k, h);
+    x = (l > k) ? x - a[k] * yk : x;
   }
   x = x * dinv;
   SYNC();
@@ -535,20 +580,10 @@ __device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], 
   for (int k = 1; k < NV; ++k) col[k] = s.x.L[k][li];
 #pragma unroll
   for (int k = NV - 1; k > 0; --k) {
-    const float xk = rlane(x, k);
-    x = (lane < k) ? x - col[k] * xk : x;
+    const float xk = hb(x, k, h);
+    x = (l < k) ? x - col[k] * xk : x;
   }
   return x;  // callers SYNC before s.x is rewritten
-}
-
-// a[j] += w . Jc[.][j] over the columns of support SUP (0..3: base + leg SUP, 4: base, 5: all)
-template <int SUP>
-__device__ __forceinline__ void hess_acc(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
-#pragma unroll
-  for (int j = 0; j < NV; j++) {
-    const bool in = SUP == 5 || j < 6 || (SUP < 4 && j >= 6 + 3 * SUP && j < 9 + 3 * SUP);
-    if (in) a[j] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
-  }
 }
 
 // J row r dotted with x (LDS vector)
@@ -567,6 +602,13 @@ __device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float
   return a + sg * s.con_mu[c] * b;
 }
 
+// a[j] += w . J[.][j] over the columns [J0, J1) (base: 0..6, leg g: 6+3g..9+3g, dense: 0..18)
+template <int J0, int J1>
+__device__ __forceinline__ void hess_acc(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
+#pragma unroll
+  for (int j = J0; j < J1; j++) a[j] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
+}
+
 // index drawn by jax.random.choice(p) from u = uniform(key): searchsorted_left(cumsum(p), cumsum[-1]*(1-u))
 __device__ __forceinline__ int choice_from_uniform(const float* dist, int n, float u) {
   float total = 0.0f;
@@ -583,38 +625,39 @@ __device__ __forceinline__ int choice_from_uniform(const float* dist, int n, flo
 
 // ------------------------------------------------------------------------------------
 // one physics substep (mj_step): forward + Newton + Euler.  `integrate` = false for reset
-// (mj_forward only).  Must be called by all 64 lanes.
+// (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int lane, bool integrate) {
-  kinematics(s, m, lane);
+__device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate) {
+  constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
+  kinematics(s, m, l);
   SYNC();
   PHASE(0);
-  com_pos(s, m, lane);
+  com_pos(s, m, l, h);
   SYNC();
   PHASE(1);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
-  crb_times_cdof(s, m, lane);
-  rne_chain(s, m, lane);
-  collision(s, m, lane);
+  crb_times_cdof(s, m, l);
+  rne_chain(s, m, l);
+  collision(s, m, l, h);
   {
     // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
     bool act = false;
     float value = 0;
     int j = 0;
-    if (lane < 2 * (NJ - 1)) {
-      j = 1 + (lane >> 1);
-      const int side = (lane & 1) ? 1 : -1;
+    if (l < 2 * (NJ - 1)) {
+      j = 1 + (l >> 1);
+      const int side = (l & 1) ? 1 : -1;
       if (m.jnt_limited[j]) {
         value = side * (m.jnt_range[j][(side + 1) / 2] - s.qpos[7 + j - 1]);
         act = value < m.lim_margin[j];
       }
     }
-    const uint64_t mask = __ballot(act);
-    const int slot = __popcll(mask & ((1ull << lane) - 1ull));
+    const uint32_t mask = hballot(act, h);
+    const int slot = __popc(mask & ((1u << l) - 1u));
     if (act) {
       const int dof = 6 + j - 1;
-      const float sg = (lane & 1) ? -1.0f : 1.0f;  // J = -side
+      const float sg = (l & 1) ? -1.0f : 1.0f;  // J = -side
       s.lim_dof[slot] = dof;
       s.lim_sgn[slot] = sg;
       const float imp = getimp(m.lim_solimp[j], value, m.lim_margin[j]);
@@ -624,32 +667,32 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
       s.efc_D[r] = 1.0f / R;
       s.efc_aref[r] = -m.lim_b[j] * (sg * s.qvel[dof]) - m.lim_k[j] * imp * (value - m.lim_margin[j]);
     }
-    if (lane == 0) s.nl = __popcll(mask);
-    if (lane < NFR) {  // dof frictionloss rows (R, b precomputed: pos = 0)
-      const int dof = 6 + lane;
-      s.efc_R[lane] = m.fr_R[dof];
-      s.efc_D[lane] = 1.0f / m.fr_R[dof];
-      s.efc_aref[lane] = -m.fr_b[dof] * s.qvel[dof];
+    if (l == 0) s.nl = __popc(mask);
+    if (l < NFR) {  // dof frictionloss rows (R, b precomputed: pos = 0)
+      const int dof = 6 + l;
+      s.efc_R[l] = m.fr_R[dof];
+      s.efc_D[l] = 1.0f / m.fr_R[dof];
+      s.efc_aref[l] = -m.fr_b[dof] * s.qvel[dof];
     }
-    if (lane < NU) {  // actuation (affine PD + force clamp)
-      const int d = m.act_dof[lane];
-      float ctrl = s.ctrl[lane];
-      if (m.act_ctrllimited[lane]) ctrl = fminf(fmaxf(ctrl, m.act_crange[lane][0]), m.act_crange[lane][1]);
-      const float gear = m.act_gear[lane];
-      const float len = gear * s.qpos[m.act_qadr[lane]], vel = gear * s.qvel[d];
-      float gain = m.act_gain[lane], b0 = m.act_bias[lane][0], b1 = m.act_bias[lane][1], b2 = m.act_bias[lane][2];
+    if (l < NU) {  // actuation (affine PD + force clamp)
+      const int d = m.act_dof[l];
+      float ctrl = s.ctrl[l];
+      if (m.act_ctrllimited[l]) ctrl = fminf(fmaxf(ctrl, m.act_crange[l][0]), m.act_crange[l][1]);
+      const float gear = m.act_gear[l];
+      const float len = gear * s.qpos[m.act_qadr[l]], vel = gear * s.qvel[d];
+      float gain = m.act_gain[l], b0 = m.act_bias[l][0], b1 = m.act_bias[l][1], b2 = m.act_bias[l][2];
       if (s.dr_on) { gain = s.kp; b1 = -s.kp; b2 = -s.kd; }
       float force = gain * ctrl;
-      if (m.act_biastype[lane] == PP3_BIAS_AFFINE) force += b0 + b1 * len + b2 * vel;
-      if (m.act_forcelimited[lane]) force = fminf(fmaxf(force, m.act_frange[lane][0]), m.act_frange[lane][1]);
+      if (m.act_biastype[l] == PP3_BIAS_AFFINE) force += b0 + b1 * len + b2 * vel;
+      if (m.act_forcelimited[l]) force = fminf(fmaxf(force, m.act_frange[l][0]), m.act_frange[l][1]);
       s.qfrc_act[d] = gear * force;
     }
-    if (lane < 6) s.qfrc_act[lane] = 0.0f;
+    if (l < 6) s.qfrc_act[l] = 0.0f;
   }
   SYNC();
   PHASE(2);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
-  for (int p = lane; p < m.nmpair; p += WAVE) {
+  for (int p = l; p < m.nmpair; p += HW) {
     const int i = m.mp_i[p], j = m.mp_j[p];
     float v = 0;
 #pragma unroll
@@ -658,9 +701,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
     s.M[i][j] = v;
     s.M[j][i] = v;
   }
-  rne_body_forces(s, lane);
+  rne_body_forces(s, l, h);
   const int ncon = s.ncon;
-  for (int it = lane; it < ncon * NV; it += WAVE) {
+  for (int it = l; it < ncon * NV; it += HW) {
     const int c = it / NV, i = it - c * NV;
     const int p = s.con_pair[c];
     const int b1 = m.cg_body[m.pair_g1[p]], b2 = m.cg_body[m.pair_g2[p]];
@@ -679,13 +722,13 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
   SYNC();
   PHASE(3);
   // ---- phase 5: qfrc_bias/smooth (subtree sums of body forces), contact edge rows ----
-  if (lane < NV) {
+  if (l < NV) {
     float cf[6];
-    if (lane < 6) {
+    if (l < 6) {
 #pragma unroll
       for (int k = 0; k < 6; k++) cf[k] = s.cfrc_base[k];
     } else {  // subtree of a leg link: itself + the (<= 2) links below (cacc holds cfrc now)
-      const int b = m.dof_body[lane], last = 2 + 3 * ((b - 2) / 3) + 2;
+      const int b = m.dof_body[l], last = 2 + 3 * ((b - 2) / 3) + 2;
 #pragma unroll
       for (int k = 0; k < 6; k++) cf[k] = s.x.a.cacc[b][k];
 #pragma unroll
@@ -697,12 +740,12 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
       }
     }
     float bias = 0;
-    for (int k = 0; k < 6; k++) bias += s.cdof[lane][k] * cf[k];
-    s.qfrc_smooth[lane] = -m.dof_damping[lane] * s.qvel[lane] - bias + s.qfrc_act[lane];
+    for (int k = 0; k < 6; k++) bias += s.cdof[l][k] * cf[k];
+    s.qfrc_smooth[l] = -m.dof_damping[l] * s.qvel[l] - bias + s.qfrc_act[l];
   }
   const int nl = s.nl;
   const int nefc = NFR + nl + 4 * ncon;
-  for (int e = lane; e < 4 * ncon; e += WAVE) {
+  for (int e = l; e < 4 * ncon; e += HW) {
     const int c = e >> 2, p = s.con_pair[c], r = NFR + nl + e;
     const float mu = s.con_mu[c];
     const float dist = s.con_dist[c];
@@ -718,24 +761,24 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
   SYNC();
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
   {
-    const int li = lane < NV ? lane : NV - 1;
+    const int li = l < NV ? l : NV - 1;
     float a[NV], dinv = 1.0f;
 #pragma unroll
     for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
-    ldl_rows_lds(a, dinv, lane, &s.x.L[0][0]);
-    const float x = ldl_solve(s, a, dinv, s.qfrc_smooth[li], lane);
-    if (lane < NV) s.qacc_smooth[lane] = x;
+    ldl_rows(a, dinv, l, &s.x.L[0][0]);
+    const float x = ldl_solve(s, a, dinv, s.qfrc_smooth[li], l, h);
+    if (l < NV) s.qacc_smooth[l] = x;
   }
   SYNC();
   PHASE(4);
 
   // ---- phase 7: Newton solver (mj_solNewton), warm-started ----
-  // per-lane rows r0 = lane, r1 = lane + 64
-  float Dr[2], Rr[2], ar[2], fl[2];
-  bool valid[2], isfr[2];
+  // per-lane rows r = l + HW * t
+  float Dr[NR], Rr[NR], ar[NR], fl[NR];
+  bool valid[NR], isfr[NR];
 #pragma unroll
-  for (int t = 0; t < 2; t++) {
-    const int r = lane + WAVE * t;
+  for (int t = 0; t < NR; t++) {
+    const int r = l + HW * t;
     valid[t] = r < nefc;
     isfr[t] = r < NFR;
     Dr[t] = valid[t] ? s.efc_D[r] : 0.0f;
@@ -744,12 +787,12 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
     fl[t] = (valid[t] && isfr[t]) ? m.fr_floss[6 + r] : 0.0f;
   }
   // warm start: total cost at qacc_warmstart vs at qacc_smooth
+  float cws = 0, csm = 0;
   {
-    float cws = 0, csm = 0;
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+    for (int t = 0; t < NR; t++) {
       if (!valid[t]) continue;
-      const int r = lane + WAVE * t;
+      const int r = l + HW * t;
       const float x1 = row_dot(s, r, s.qws) - ar[t];
       const float x2 = row_dot(s, r, s.qacc_smooth) - ar[t];
       if (isfr[t]) {
@@ -761,33 +804,35 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
         csm += (x2 < 0) ? 0.5f * Dr[t] * x2 * x2 : 0.0f;
       }
     }
-    if (lane < NV) {
+    if (l < NV) {
       float ma = 0;
 #pragma unroll
-      for (int j = 0; j < NV; j++) ma += s.M[lane][j] * s.qws[j];
-      cws += 0.5f * (ma - s.qfrc_smooth[lane]) * (s.qws[lane] - s.qacc_smooth[lane]);
+      for (int j = 0; j < NV; j++) ma += s.M[l][j] * s.qws[j];
+      cws += 0.5f * (ma - s.qfrc_smooth[l]) * (s.qws[l] - s.qacc_smooth[l]);
     }
-    cws = wave_sum(cws);
-    csm = wave_sum(csm);
+    cws = hsum(cws, h);
+    csm = hsum(csm, h);
     const bool use_smooth = cws > csm;
-    if (lane < NV) s.qacc[lane] = use_smooth ? s.qacc_smooth[lane] : s.qws[lane];
+    if (l < NV) s.qacc[l] = use_smooth ? s.qacc_smooth[l] : s.qws[l];
   }
   SYNC();
   PHASE(5);
+  const int cmax = wmax2(ncon);
+  bool live = true;  // this env still iterating (per half)
   for (int iter = 0; iter < m.iterations; iter++) {
     // Ma, Jaref, constraint state/force
     float ma = 0;
-    if (lane < NV) {
+    if (l < NV) {
 #pragma unroll
-      for (int j = 0; j < NV; j++) ma += s.M[lane][j] * s.qacc[j];
-      s.Ma[lane] = ma;
+      for (int j = 0; j < NV; j++) ma += s.M[l][j] * s.qacc[j];
+      s.Ma[l] = ma;
     }
-    float jar[2];
+    float jar[NR];
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+    for (int t = 0; t < NR; t++) {
       jar[t] = 0;
       if (!valid[t]) continue;
-      const int r = lane + WAVE * t;
+      const int r = l + HW * t;
       const float x = row_dot(s, r, s.qacc) - ar[t];
       jar[t] = x;
       float f, Dq = 0.0f;
@@ -806,24 +851,24 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
     SYNC();
     // gradient, diagonal D per dof, contact Hessian blocks
     float gauss = 0;
-    if (lane < NV) {
+    if (l < NV) {
       float qc = 0;
-      if (lane >= 6) qc += s.efc_force[lane - 6];
-      float dD = (lane >= 6) ? s.efc_D[lane - 6] : 0.0f;
+      if (l >= 6) qc += s.efc_force[l - 6];
+      float dD = (l >= 6) ? s.efc_D[l - 6] : 0.0f;
       for (int i = 0; i < nl; i++)
-        if (s.lim_dof[i] == lane) { qc += s.lim_sgn[i] * s.efc_force[NFR + i]; dD += s.efc_D[NFR + i]; }
+        if (s.lim_dof[i] == l) { qc += s.lim_sgn[i] * s.efc_force[NFR + i]; dD += s.efc_D[NFR + i]; }
       for (int c = 0; c < ncon; c++) {
         const int r = NFR + nl + 4 * c;
         const float f0 = s.efc_force[r], f1 = s.efc_force[r + 1], f2 = s.efc_force[r + 2], f3 = s.efc_force[r + 3];
         const float mu = s.con_mu[c];
-        qc += s.Jc[c][0][lane] * (f0 + f1 + f2 + f3) + mu * s.Jc[c][1][lane] * (f0 - f1) + mu * s.Jc[c][2][lane] * (f2 - f3);
+        qc += s.Jc[c][0][l] * (f0 + f1 + f2 + f3) + mu * s.Jc[c][1][l] * (f0 - f1) + mu * s.Jc[c][2][l] * (f2 - f3);
       }
-      s.grad[lane] = ma - s.qfrc_smooth[lane] - qc;
-      s.dofD[lane] = dD;
-      gauss = 0.5f * (ma - s.qfrc_smooth[lane]) * (s.qacc[lane] - s.qacc_smooth[lane]);
+      s.grad[l] = ma - s.qfrc_smooth[l] - qc;
+      s.dofD[l] = dD;
+      gauss = 0.5f * (ma - s.qfrc_smooth[l]) * (s.qacc[l] - s.qacc_smooth[l]);
     }
-    if (lane >= 32 && lane < 32 + ncon) {
-      const int c = lane - 32, r = NFR + nl + 4 * c;
+    for (int c = l; c < ncon; c += HW) {
+      const int r = NFR + nl + 4 * c;
       const float mu = s.con_mu[c];
       const float d0 = s.efc_D[r], d1 = s.efc_D[r + 1], d2 = s.efc_D[r + 2], d3 = s.efc_D[r + 3];
       s.con_G[c][0] = d0 + d1 + d2 + d3;
@@ -832,65 +877,81 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
       s.con_G[c][3] = mu * mu * (d0 + d1);
       s.con_G[c][4] = mu * mu * (d2 + d3);
     }
-    gauss = wave_sum(gauss);
+    gauss = hsum(gauss, h);
     SYNC();
     PHASE(6);
     // Hessian rows H = M + J' D J (registers), LDL^T, search = -H^-1 grad
     {
-      const int li = lane < NV ? lane : NV - 1;
+      const int li = l < NV ? l : NV - 1;
       float a[NV], dinv = 1.0f;
 #pragma unroll
       for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
       const float dD = s.dofD[li];
 #pragma unroll
       for (int j = 0; j < NV; j++) a[j] += (j == li) ? dD : 0.0f;
-      for (int c = 0; c < ncon; c++) {
-        const float* G = s.con_G[c];
-        const float jn = s.Jc[c][0][li], j1 = s.Jc[c][1][li], j2 = s.Jc[c][2][li];
-        const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
-        const float w1 = jn * G[1] + j1 * G[3];
-        const float w2 = jn * G[2] + j2 * G[4];
+      for (int c = 0; c < cmax; c++) {
+        const bool cv = c < ncon;
         // J' D J only over the Jacobian's column support (base + one leg for robot-vs-static
-        // contacts): a wave-uniform switch instead of 18 dense columns
-        switch (__builtin_amdgcn_readfirstlane(s.con_sup[c])) {
-          case 0: hess_acc<0>(a, s.Jc[c], w0, w1, w2); break;
-          case 1: hess_acc<1>(a, s.Jc[c], w0, w1, w2); break;
-          case 2: hess_acc<2>(a, s.Jc[c], w0, w1, w2); break;
-          case 3: hess_acc<3>(a, s.Jc[c], w0, w1, w2); break;
-          case 4: hess_acc<4>(a, s.Jc[c], w0, w1, w2); break;
-          default: hess_acc<5>(a, s.Jc[c], w0, w1, w2); break;
+        // contacts); the union over the wave's two envs is a wave-uniform choice
+        const int sup = cv ? s.con_sup[c] : 4;
+        const int sa = __builtin_amdgcn_readlane(sup, 0), sb = __builtin_amdgcn_readlane(sup, HW);
+        if (cv) {
+          const float* G = s.con_G[c];
+          const float jn = s.Jc[c][0][li], j1 = s.Jc[c][1][li], j2 = s.Jc[c][2][li];
+          const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
+          const float w1 = jn * G[1] + j1 * G[3];
+          const float w2 = jn * G[2] + j2 * G[4];
+          if (sa == 5 || sb == 5) {
+            hess_acc<0, NV>(a, s.Jc[c], w0, w1, w2);
+          } else {
+            hess_acc<0, 6>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 0 || sb == 0) hess_acc<6, 9>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 1 || sb == 1) hess_acc<9, 12>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 2 || sb == 2) hess_acc<12, 15>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 3 || sb == 3) hess_acc<15, 18>(a, s.Jc[c], w0, w1, w2);
+          }
         }
       }
-      ldl_rows_lds(a, dinv, lane, &s.x.L[0][0]);
-      const float x = ldl_solve(s, a, dinv, s.grad[li], lane);
-      if (lane < NV) s.search[lane] = -x;
+#ifdef PP3_DEBUG
+      if (blockIdx.x == 0 && h == 0 && l < NV)
+        for (int j = 0; j < NV; j++) g_dbg[64 + NV * l + j] = a[j];
+      if (blockIdx.x == 0 && h == 0 && l >= 12 && l < 20) {
+        g_dbg[400 + l - 12] = s.efc_D[l];
+        g_dbg[430 + l - 12] = jar[0];
+        g_dbg[440 + l - 12] = s.efc_force[l];
+      }
+      if (blockIdx.x == 0 && h == 0 && l < 10) g_dbg[410 + l] = s.con_G[l / 5][l % 5];
+#endif
+      ldl_rows(a, dinv, l, &s.x.L[0][0]);
+      const float x = ldl_solve(s, a, dinv, s.grad[li], l, h);
+      if (l < NV) s.search[l] = -x;
     }
     SYNC();
     PHASE(7);
     // line-search quadratics (Gauss part) and search-direction norm
     float q1 = 0, q2 = 0, sn = 0;
-    if (lane < NV) {
-      const float sv = s.search[lane];
+    if (l < NV) {
+      const float sv = s.search[l];
       float mv = 0;
 #pragma unroll
-      for (int j = 0; j < NV; j++) mv += s.M[lane][j] * s.search[j];
-      q1 = sv * (s.Ma[lane] - s.qfrc_smooth[lane]);
+      for (int j = 0; j < NV; j++) mv += s.M[l][j] * s.search[j];
+      q1 = sv * (s.Ma[l] - s.qfrc_smooth[l]);
       q2 = 0.5f * sv * mv;
       sn = sv * sv;
     }
-    q1 = wave_sum(q1);
-    q2 = wave_sum(q2);
-    sn = sqrtf(wave_sum(sn));
-    if (sn < MINVAL) break;
-    float jv[2];
+    q1 = hsum(q1, h);
+    q2 = hsum(q2, h);
+    sn = sqrtf(hsum(sn, h));
+    live = live && !(sn < MINVAL);
+    float jv[NR];
 #pragma unroll
-    for (int t = 0; t < 2; t++) jv[t] = valid[t] ? row_dot(s, lane + WAVE * t, s.search) : 0.0f;
+    for (int t = 0; t < NR; t++) jv[t] = valid[t] ? row_dot(s, l + HW * t, s.search) : 0.0f;
     const float gtol = m.gtol_scale * sn;
     // cost and derivatives of the 1-D piecewise quadratic at alpha
     auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
       float t0 = 0, t1 = 0, t2 = 0;
 #pragma unroll
-      for (int t = 0; t < 2; t++) {
+      for (int t = 0; t < NR; t++) {
         if (!valid[t]) continue;
         const float x = jar[t] + alpha * jv[t];
         const float D = Dr[t];
@@ -905,18 +966,19 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
         t1 += D * jar[t] * jv[t];
         t2 += 0.5f * D * jv[t] * jv[t];
       }
-      t0 = wave_sum(t0) + gauss;
-      t1 = wave_sum(t1) + q1;
-      t2 = wave_sum(t2) + q2;
+      t0 = hsum(t0, h) + gauss;
+      t1 = hsum(t1, h) + q1;
+      t2 = hsum(t2, h) + q2;
       cost = t0 + alpha * t1 + alpha * alpha * t2;
       d0 = t1 + 2.0f * alpha * t2;
       d1 = fmaxf(2.0f * t2, MINVAL);
     };
-    // PrimalSearch-style exact line search (same control flow as the oracle)
+    // PrimalSearch-style exact line search (same control flow as the oracle); every branch
+    // below is per env (per half), the wave runs the union of both envs' evaluations
+    float alpha = 0.0f;
     int evals = 0;
-    const int maxit = m.ls_iterations;
-    float alpha;
-    {
+    if (live) {
+      const int maxit = m.ls_iterations;
       float c0, g0, h0;
       eval(0.0f, c0, g0, h0);
       evals++;
@@ -941,7 +1003,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
           alpha = a1;
         } else {
           // bracket [p2, p1]; candidates p1next, p2next (= p1 initially), midpoint
-          float a2n = a1, c2n = c1, g2n = g1;
+          float a2n = a1, c2n = c1, g2n = g1, h2n = h1;
           float a1n = a1 - g1 / h1, c1n, g1n, h1n;
           eval(a1n, c1n, g1n, h1n);
           evals++;
@@ -967,41 +1029,50 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
   if (g1 * (CG) > 0 && fabsf(CG) < fabsf(g1)) { a1 = CA; c1 = CC; g1 = CG; h1 = CH; up1 = true; } \
   if (g2 * (CG) > 0 && fabsf(CG) < fabsf(g2)) { a2 = CA; c2 = CC; g2 = CG; h2 = CH; up2 = true; }
             PP3_TIGHTEN(a1n, c1n, g1n, h1n)
-            PP3_TIGHTEN(a2n, c2n, g2n, h1)
+            PP3_TIGHTEN(a2n, c2n, g2n, h2n)
             PP3_TIGHTEN(am, cm, gm, hm)
 #undef PP3_TIGHTEN
             if (!up1 && !up2) break;
             if (up1) { a1n = a1 - g1 / h1; eval(a1n, c1n, g1n, h1n); evals++; }
-            if (up2) { float hh; a2n = a2 - g2 / h2; eval(a2n, c2n, g2n, hh); evals++; }
+            if (up2) { a2n = a2 - g2 / h2; eval(a2n, c2n, g2n, h2n); evals++; }
           }
           if (!finished) alpha = c1 < c2 ? a1 : a2;
         }
       }
     }
     PHASE(8);
-    if (alpha == 0.0f) break;
-    if (lane < NV) s.qacc[lane] += alpha * s.search[lane];
+#ifdef PP3_DEBUG
+    if (blockIdx.x == 0 && h == 0) {
+      if (l < NV) { g_dbg[l] = s.qacc[l]; g_dbg[18 + l] = s.grad[l]; g_dbg[36 + l] = s.search[l]; }
+      if (l == 0) {
+        g_dbg[54] = gauss; g_dbg[55] = q1; g_dbg[56] = q2; g_dbg[57] = sn; g_dbg[58] = gtol;
+        g_dbg[59] = alpha; g_dbg[60] = (float)evals; g_dbg[61] = cws; g_dbg[62] = csm; g_dbg[63] = (float)nefc;
+      }
+    }
+#endif
+    live = live && alpha != 0.0f;
+    if (live && l < NV) s.qacc[l] += alpha * s.search[l];
     SYNC();
   }
-  if (lane < NV) s.qws[lane] = s.qacc[lane];
+  if (l < NV) s.qws[l] = s.qacc[l];
   SYNC();
   if (!integrate) return;
   // ---- phase 8: Euler (eulerdamp disabled) ----
-  const float h = m.h;
+  const float hstep = m.h;
   float vn = 0;
   float w[3] = {0, 0, 0};
-  if (lane < NV) vn = s.qvel[lane] + h * s.qacc[lane];
-  if (lane == 3)
-    for (int k = 0; k < 3; k++) w[k] = s.qvel[3 + k] + h * s.qacc[3 + k];
+  if (l < NV) vn = s.qvel[l] + hstep * s.qacc[l];
+  if (l == 3)
+    for (int k = 0; k < 3; k++) w[k] = s.qvel[3 + k] + hstep * s.qacc[3 + k];
   SYNC();
-  if (lane < NV) s.qvel[lane] = vn;
-  if (lane < 3) s.qpos[lane] += h * vn;
-  if (lane >= 6 && lane < NV) s.qpos[lane + 1] += h * vn;
-  if (lane == 3) {
+  if (l < NV) s.qvel[l] = vn;
+  if (l < 3) s.qpos[l] += hstep * vn;
+  if (l >= 6 && l < NV) s.qpos[l + 1] += hstep * vn;
+  if (l == 3) {
     const float n = sqrtf(dot3(w, w));
     if (n < MINVAL) { w[0] = 1; w[1] = 0; w[2] = 0; } else { const float in = 1.0f / n; w[0] *= in; w[1] *= in; w[2] *= in; }
     float qr[4], q[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
-    axisangle2quat(qr, w, h * n);
+    axisangle2quat(qr, w, hstep * n);
     normalize4(q);
     mulquat(q, q, qr);
     for (int k = 0; k < 4; k++) s.qpos[3 + k] = q[k];
@@ -1014,62 +1085,58 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int la
 // environment helpers
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void load_params(Shared<NC>& s, const DevModel& m, const float* dr, int lane) {
-  if (lane < NB) {
-    s.mass[lane] = dr ? dr[PP3_DR_MASS + lane] : m.body_mass[lane];
+__device__ __forceinline__ void load_params(Shared<NC>& s, const DevModel& m, const float* dr, int l) {
+  if (l < NB) {
+    s.mass[l] = dr ? dr[PP3_DR_MASS + l] : m.body_mass[l];
     for (int k = 0; k < 3; k++) {
-      s.inertia[lane][k] = dr ? dr[PP3_DR_INERTIA + 3 * lane + k] : m.body_inertia[lane][k];
-      s.ipos[lane][k] = (dr && lane == 1) ? dr[PP3_DR_BASE_IPOS + k] : m.body_ipos[lane][k];
+      s.inertia[l][k] = dr ? dr[PP3_DR_INERTIA + 3 * l + k] : m.body_inertia[l][k];
+      s.ipos[l][k] = (dr && l == 1) ? dr[PP3_DR_BASE_IPOS + k] : m.body_ipos[l][k];
     }
   }
-  if (lane == 0) {
+  if (l == 0) {
     s.dr_on = dr != nullptr;
     s.fric = dr ? dr[PP3_DR_FRICTION] : 0.0f;
     s.kp = dr ? dr[PP3_DR_KP] : 0.0f;
     s.kd = dr ? dr[PP3_DR_KD] : 0.0f;
   }
   // zero M once per launch (its sparsity pattern is fixed)
-  for (int i = lane; i < NV * (NV + 1); i += WAVE) (&s.M[0][0])[i] = 0.0f;
-}
-
-__device__ __forceinline__ Key bcast_key(Key k, int l) {
-  return Key{(uint32_t)__builtin_amdgcn_readlane((int)k.a, l), (uint32_t)__builtin_amdgcn_readlane((int)k.b, l)};
+  for (int i = l; i < NV * (NV + 1); i += HW) (&s.M[0][0])[i] = 0.0f;
 }
 
 // sample_lagged_value on one buffer row in HBM (utils.py:34-69): push `v` to the front of
 // row[0..n), return the value now at column li.  Register-staged (read all, then write).
-__device__ __forceinline__ float push_lagged(float* row, int n, float v, int li) {
+__device__ __forceinline__ float push_lagged(float* row, int n, float v, int li, bool store) {
   float old[PP3_MAX_LAG];
 #pragma unroll
-  for (int l = 0; l < PP3_MAX_LAG; l++) old[l] = l < n ? row[l] : 0.0f;
+  for (int q = 0; q < PP3_MAX_LAG; q++) old[q] = q < n ? row[q] : 0.0f;
   float out = v;
 #pragma unroll
-  for (int l = 0; l < PP3_MAX_LAG; l++) {
-    const float nv = l == 0 ? v : old[l - 1];
-    if (l < n) row[l] = nv;
-    out = (l == li) ? nv : out;
+  for (int q = 0; q < PP3_MAX_LAG; q++) {
+    const float nv = q == 0 ? v : old[q - 1];
+    if (store && q < n) row[q] = nv;
+    out = (q == li) ? nv : out;
   }
   return out;
 }
 
 // sample_command (environment.py:246-272): lanes 0..6 draw, lane 0 writes out[3]
-__device__ __forceinline__ void sample_command(const DevModel& m, Key rng, float* out, int lane) {
+__device__ __forceinline__ void sample_command(const DevModel& m, Key rng, float* out, int l, int h) {
   const int part = m.partitionable;
   float u = 0;
-  if (lane < 3) {
-    const Key k = split_i(rng, 6, 1 + lane, part);
-    const float lo = lane == 0 ? m.cmd_x[0] : lane == 1 ? m.cmd_y[0] : m.cmd_w[0];
-    const float hi = lane == 0 ? m.cmd_x[1] : lane == 1 ? m.cmd_y[1] : m.cmd_w[1];
+  if (l < 3) {
+    const Key k = split_i(rng, 6, 1 + l, part);
+    const float lo = l == 0 ? m.cmd_x[0] : l == 1 ? m.cmd_y[0] : m.cmd_w[0];
+    const float hi = l == 0 ? m.cmd_x[1] : l == 1 ? m.cmd_y[1] : m.cmd_w[1];
     u = uniform_i(k, 1, 0, lo, hi, part);
-  } else if (lane == 3) {
+  } else if (l == 3) {
     u = uniform_i(split_i(rng, 6, 4, part), 1, 0, 0.0f, 1.0f, part);
-  } else if (lane < 7) {
-    u = uniform_i(split_i(rng, 6, 5, part), 3, lane - 4, -m.stand_thr, m.stand_thr, part);
+  } else if (l < 7) {
+    u = uniform_i(split_i(rng, 6, 5, part), 3, l - 4, -m.stand_thr, m.stand_thr, part);
   }
-  const bool zero = rlane(u, 3) < m.zero_cmd_p;
-  const float c0 = rlane(u, 0), c1 = rlane(u, 1), c2 = rlane(u, 2);
-  const float z0 = rlane(u, 4), z1 = rlane(u, 5), z2 = rlane(u, 6);
-  if (lane == 0) {
+  const bool zero = hb(u, 3, h) < m.zero_cmd_p;
+  const float c0 = hb(u, 0, h), c1 = hb(u, 1, h), c2 = hb(u, 2, h);
+  const float z0 = hb(u, 4, h), z1 = hb(u, 5, h), z2 = hb(u, 6, h);
+  if (l == 0) {
     out[0] = zero ? z0 : c0;
     out[1] = zero ? z1 : c1;
     out[2] = zero ? z2 : c2;
@@ -1077,13 +1144,13 @@ __device__ __forceinline__ void sample_command(const DevModel& m, Key rng, float
 }
 
 // sample_body_orientation (environment.py:274-298), brax math.euler_to_quat (degrees)
-__device__ __forceinline__ void sample_orientation(const DevModel& m, Key rng, float* out, int lane) {
+__device__ __forceinline__ void sample_orientation(const DevModel& m, Key rng, float* out, int l, int h) {
   const int part = m.partitionable;
   float u = 0;
-  if (lane < 2) u = uniform_i(split_i(rng, 3, 1 + lane, part), 1, 0, -1.0f, 1.0f, part);
-  const float pitch = rlane(u, 0) * m.max_pitch;
-  const float roll = rlane(u, 1) * m.max_roll;
-  if (lane == 0) {
+  if (l < 2) u = uniform_i(split_i(rng, 3, 1 + l, part), 1, 0, -1.0f, 1.0f, part);
+  const float pitch = hb(u, 0, h) * m.max_pitch;
+  const float roll = hb(u, 1, h) * m.max_roll;
+  if (l == 0) {
     const float pi = m.pi_f;
     const float c1 = cosf(roll * pi / 360.0f), c2 = cosf(pitch * pi / 360.0f), c3 = 1.0f;
     const float s1 = sinf(roll * pi / 360.0f), s2 = sinf(pitch * pi / 360.0f), s3 = 0.0f;
@@ -1098,24 +1165,24 @@ __device__ __forceinline__ void sample_orientation(const DevModel& m, Key rng, f
 // _get_obs (environment.py:485-543): consumes the st rng, pushes the IMU buffer (HBM row
 // gimu = [6][Li]), writes s.x.e.o[36]
 template <int NC>
-__device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int lane) {
+__device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int l, int h, bool store) {
   const int part = m.partitionable;
   const Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
-  const Key kl = split_i(rng, 6, lane < 6 ? lane : 0, part);  // lane i holds split(rng, 6)[i]
-  const Key k0 = bcast_key(kl, 0), ka = bcast_key(kl, 1), kg = bcast_key(kl, 2);
-  const Key km = bcast_key(kl, 3), kla = bcast_key(kl, 4), ki = bcast_key(kl, 5);
+  const Key kl = split_i(rng, 6, l < 6 ? l : 0, part);  // lane i holds split(rng, 6)[i]
+  const Key k0 = hkey(kl, 0, h), ka = hkey(kl, 1, h), kg = hkey(kl, 2, h);
+  const Key km = hkey(kl, 3, h), kla = hkey(kl, 4, h), ki = hkey(kl, 5, h);
   // noise draws: 0-2 ang, 3-5 grav, 6-17 motor, 18-29 last act, 30 imu choice
-  if (lane < 31) {
-    const Key kk = lane < 3 ? ka : lane < 6 ? kg : lane < 18 ? km : lane < 30 ? kla : ki;
-    const int cnt = lane < 6 ? 3 : lane < 30 ? 12 : 1;
-    const int idx = lane < 3 ? lane : lane < 6 ? lane - 3 : lane < 18 ? lane - 6 : lane < 30 ? lane - 18 : 0;
-    const float scale = lane < 3 ? m.n_ang : lane < 6 ? m.n_grav : lane < 18 ? m.n_motor : lane < 30 ? m.n_act : 1.0f;
-    const float lo = lane < 30 ? -1.0f : 0.0f;
+  if (l < 31) {
+    const Key kk = l < 3 ? ka : l < 6 ? kg : l < 18 ? km : l < 30 ? kla : ki;
+    const int cnt = l < 6 ? 3 : l < 30 ? 12 : 1;
+    const int idx = l < 3 ? l : l < 6 ? l - 3 : l < 18 ? l - 6 : l < 30 ? l - 18 : 0;
+    const float scale = l < 3 ? m.n_ang : l < 6 ? m.n_grav : l < 18 ? m.n_motor : l < 30 ? m.n_act : 1.0f;
+    const float lo = l < 30 ? -1.0f : 0.0f;
     const float v = uniform_i(kk, cnt, idx, lo, 1.0f, part);
-    s.x.e.u[lane] = lane < 30 ? v * scale : v;
+    s.x.e.u[l] = l < 30 ? v * scale : v;
   }
   SYNC();
-  if (lane < 6) {  // one IMU channel per lane
+  if (l < 6) {  // one IMU channel per lane
     float inv[4] = {1, 0, 0, 0}, angl[3] = {0, 0, 0};
     if (m.use_imu) {
       inv[0] = s.xquat[1][0]; inv[1] = -s.xquat[1][1]; inv[2] = -s.xquat[1][2]; inv[3] = -s.xquat[1][3];
@@ -1126,22 +1193,22 @@ __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float*
     b_rotate(g, g0, inv);
     for (int k = 0; k < 3; k++) g[k] += s.x.e.u[3 + k];
     const float gn = sqrtf(dot3(g, g));
-    const float v = lane < 3 ? angl[lane] + s.x.e.u[lane] : g[lane - 3] / gn;
+    const float v = l < 3 ? angl[l] + s.x.e.u[l] : g[l - 3] / gn;
     const int li = choice_from_uniform(m.imu_lat_dist, m.Li, s.x.e.u[30]);
-    const float lagged = push_lagged(gimu + lane * m.Li, m.Li, v, li);
-    s.x.e.o[lane] = fminf(fmaxf(lagged, -100.0f), 100.0f);
+    const float lagged = push_lagged(gimu + l * m.Li, m.Li, v, li, store);
+    s.x.e.o[l] = fminf(fmaxf(lagged, -100.0f), 100.0f);
   }
-  if (lane == 6) {
+  if (l == 6) {
     s.st[PP3_S_RNG] = __uint_as_float(k0.a);
     s.st[PP3_S_RNG + 1] = __uint_as_float(k0.b);
   }
-  if (lane >= 8 && lane < 11) {
-    const int k = lane - 8;
+  if (l >= 8 && l < 11) {
+    const int k = l - 8;
     s.x.e.o[6 + k] = fminf(fmaxf(s.st[PP3_S_COMMAND + k], -100.0f), 100.0f);
     s.x.e.o[9 + k] = fminf(fmaxf(s.st[PP3_S_DESIRED_Z + k], -100.0f), 100.0f);
   }
-  if (lane >= 16 && lane < 28) {
-    const int j = lane - 16;
+  if (l >= 16 && l < 28) {
+    const int j = l - 16;
     const float a = s.qpos[7 + j] - m.default_pose[j] + s.x.e.u[6 + j];
     const float b = s.st[PP3_S_LAST_ACT + j] + s.x.e.u[18 + j];
     s.x.e.o[12 + j] = fminf(fmaxf(a, -100.0f), 100.0f);
@@ -1152,25 +1219,26 @@ __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float*
 
 template <int NC>
 __device__ __forceinline__ void write_obs(Shared<NC>& s, const DevModel& m, const float* obs_in, float* obs_out,
-                                          int lane) {
+                                          int l, bool store) {
   const int nmove = PP3_OBS_DIM * (m.H - 1);
   float tmp[OBS_MOVE];
 #pragma unroll
   for (int t = 0; t < OBS_MOVE; t++) {
-    const int k = lane + WAVE * t;
+    const int k = l + HW * t;
     tmp[t] = (k < nmove && obs_in) ? obs_in[k] : 0.0f;
   }
+  if (!store) return;
 #pragma unroll
   for (int t = 0; t < OBS_MOVE; t++) {
-    const int k = lane + WAVE * t;
+    const int k = l + HW * t;
     if (k < nmove) obs_out[PP3_OBS_DIM + k] = tmp[t];
   }
-  if (lane < PP3_OBS_DIM) obs_out[lane] = s.x.e.o[lane];
+  for (int k = l; k < PP3_OBS_DIM; k += HW) obs_out[k] = s.x.e.o[k];
 }
 
 template <int NC>
-__device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int lane) {
-  for (int i = lane; i < PP3_PIPE_STRIDE; i += WAVE) {
+__device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int l) {
+  for (int i = l; i < PP3_PIPE_STRIDE; i += HW) {
     float v = 0.0f;
     if (i < PP3_P_XQUAT) { const int b = 1 + i / 3, k = i % 3; v = s.xpos[b][k]; }
     else if (i < PP3_P_XD_VEL) { const int q = i - PP3_P_XQUAT, b = 1 + q / 4, k = q % 4; v = s.xquat[b][k]; }
@@ -1195,7 +1263,8 @@ __device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m,
 }
 
 // ------------------------------------------------------------------------------------
-// kernels
+// kernels: workgroup b = one wave = envs 2b (lanes 0..31) and 2b+1 (lanes 32..63).  With an
+// odd N the last wave's second half recomputes env N-1 and stores nothing.
 // ------------------------------------------------------------------------------------
 struct StepArgs {
   const DevModel* m;
@@ -1212,38 +1281,41 @@ struct StepArgs {
 };
 
 template <int NC>
-__global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArgs a) {
-  __shared__ Shared<NC> s;
-  const int env = blockIdx.x;
+__global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
+  __shared__ Shared<NC> sh[2];
   const int lane = threadIdx.x;
-  if (env >= a.N) return;
+  const int h = lane >> 5, l = lane & (HW - 1);
+  const int env_raw = 2 * blockIdx.x + h;
+  const bool own = env_raw < a.N;
+  const int env = own ? env_raw : a.N - 1;
+  Shared<NC>& s = sh[h];
   const DevModel& m = *a.m;
   const int stride = m.stride;
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;
 #ifdef PP3_PHASE_PROF
-  if (lane < 16) s.prof[lane] = 0;
-  if (lane == 0) s.prof_t = __builtin_amdgcn_s_memtime();
+  if (l < 16) s.prof[l] = 0;
+  if (l == 0) s.prof_t = __builtin_amdgcn_s_memtime();
 #endif
-  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) s.st[i] = gst[i];
-  load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, lane);
+  for (int i = l; i < PP3_S_ACT_BUF; i += HW) s.st[i] = gst[i];
+  load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
   SYNC();
-  if (lane < NQ) s.qpos[lane] = s.st[PP3_S_QPOS + lane];
-  if (lane < NV) { s.qvel[lane] = s.st[PP3_S_QVEL + lane]; s.qws[lane] = s.st[PP3_S_QACC_WS + lane]; }
+  if (l < NQ) s.qpos[l] = s.st[PP3_S_QPOS + l];
+  if (l < NV) { s.qvel[l] = s.st[PP3_S_QVEL + l]; s.qws[l] = s.st[PP3_S_QACC_WS + l]; }
   // ---- prologue: rng split (environment.py:349), kick (:352-356), action latency (:359-365) ----
   const Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
-  const Key kl = split_i(rng, 5, lane < 5 ? lane : 0, part);  // lane i holds split(rng, 5)[i]
-  const Key k_new = bcast_key(kl, 0), cmd_key = bcast_key(kl, 1);
-  const Key kkick = bcast_key(kl, 2), kbern = bcast_key(kl, 3), klat = bcast_key(kl, 4);
+  const Key kl = split_i(rng, 5, l < 5 ? l : 0, part);  // lane i holds split(rng, 5)[i]
+  const Key k_new = hkey(kl, 0, h), cmd_key = hkey(kl, 1, h);
+  const Key kkick = hkey(kl, 2, h), kbern = hkey(kl, 3, h), klat = hkey(kl, 4, h);
   float u = 0;
-  if (lane < 4) {
-    const Key kk = lane < 2 ? kkick : (lane == 2 ? kbern : klat);
-    u = uniform_i(kk, lane < 2 ? 2 : 1, lane < 2 ? lane : 0, lane < 2 ? -1.0f : 0.0f, 1.0f, part);
+  if (l < 4) {
+    const Key kk = l < 2 ? kkick : (l == 2 ? kbern : klat);
+    u = uniform_i(kk, l < 2 ? 2 : 1, l < 2 ? l : 0, l < 2 ? -1.0f : 0.0f, 1.0f, part);
   }
-  const float bern = rlane(u, 2) < m.kick_p ? 1.0f : 0.0f;
-  const float kick0 = rlane(u, 0) * m.kick_vel * bern, kick1 = rlane(u, 1) * m.kick_vel * bern;
-  const int li = choice_from_uniform(m.lat_dist, m.La, rlane(u, 3));
-  if (lane == 0) {
+  const float bern = hb(u, 2, h) < m.kick_p ? 1.0f : 0.0f;
+  const float kick0 = hb(u, 0, h) * m.kick_vel * bern, kick1 = hb(u, 1, h) * m.kick_vel * bern;
+  const int li = choice_from_uniform(m.lat_dist, m.La, hb(u, 3, h));
+  if (l == 0) {
     s.qvel[0] += kick0;
     s.qvel[1] += kick1;
     s.st[PP3_S_KICK] = kick0;
@@ -1252,39 +1324,36 @@ __global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArg
     s.st[PP3_S_RNG + 1] = __uint_as_float(k_new.b);
   }
   const float* act_env = a.actions + (size_t)env * NU;
-  if (lane < NU) {
-    const float lagged = push_lagged(gst + PP3_S_ACT_BUF + lane * m.La, m.La, act_env[lane], li);
-    const float t = m.default_pose[lane] + lagged * m.action_scale;
-    s.ctrl[lane] = fminf(fmaxf(t, m.jlo[lane]), m.jhi[lane]);
+  if (l < NU) {
+    const float lagged = push_lagged(gst + PP3_S_ACT_BUF + l * m.La, m.La, act_env[l], li, own);
+    const float t = m.default_pose[l] + lagged * m.action_scale;
+    s.ctrl[l] = fminf(fmaxf(t, m.jlo[l]), m.jhi[l]);
   }
   SYNC();
   PHASE(10);
   // ---- physics: n_frames x mj_step (environment.py:366) ----
   for (int f = 0; f < m.n_frames; f++) {
     const DevModel* mp = a.m;
-    int ln = lane;
-    // opaque per iteration: keep model loads and lane-derived addresses inside the substep
-    // (hoisting them out of the loop costs more registers than recomputing them)
-    asm volatile("" : "+s"(mp), "+v"(ln));
-    substep(s, *mp, ln, true);
+    asm volatile("" : "+s"(mp));  // keep model loads inside the substep (no loop-carried registers)
+    substep(s, *mp, l, h, true);
   }
-  if (lane < NQ) s.st[PP3_S_QPOS + lane] = s.qpos[lane];
-  if (lane < NV) { s.st[PP3_S_QVEL + lane] = s.qvel[lane]; s.st[PP3_S_QACC_WS + lane] = s.qws[lane]; }
+  if (l < NQ) s.st[PP3_S_QPOS + l] = s.qpos[l];
+  if (l < NV) { s.st[PP3_S_QVEL + l] = s.qvel[l]; s.st[PP3_S_QACC_WS + l] = s.qws[l]; }
   SYNC();
   // ---- observation ----
-  get_obs(s, m, gst + m.imu_off, lane);
-  write_obs(s, m, a.obs_in + (size_t)env * PP3_OBS_DIM * m.H, a.obs_out + (size_t)env * PP3_OBS_DIM * m.H, lane);
+  get_obs(s, m, gst + m.imu_off, l, h, own);
+  write_obs(s, m, a.obs_in + (size_t)env * PP3_OBS_DIM * m.H, a.obs_out + (size_t)env * PP3_OBS_DIM * m.H, l, own);
   PHASE(11);
   // ---- brax x/xd, feet, done, collisions ----
-  if (lane >= 1 && lane < NB) {
-    const int b = lane;
+  if (l >= 1 && l < NB) {
+    const int b = l;
     const float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]};
     float cr[3];
     cross3(cr, s.cvel[b], off);
     for (int k = 0; k < 3; k++) { s.x.e.xdv[b][k] = s.cvel[b][3 + k] + cr[k]; s.x.e.xda[b][k] = s.cvel[b][k]; }
   }
-  if (lane >= 16 && lane < 20) {
-    const int f = lane - 16;
+  if (l >= 16 && l < 20) {
+    const int f = l - 16;
     const float cz = s.foot_xpos[f][2] - m.foot_radius;
     const int last = s.st[PP3_S_LAST_CONTACT + f] != 0.0f;
     const int c = cz < 1e-3f;
@@ -1294,7 +1363,7 @@ __global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArg
     s.x.e.first[f] = (s.st[PP3_S_AIR_TIME + f] > 0.0f && (c | last)) ? 1.0f : 0.0f;
     s.st[PP3_S_AIR_TIME + f] += m.dt;
   }
-  if (lane == 20) {
+  if (l == 20) {
     const int tb = m.torso_body;
     const float up[3] = {0, 0, 1};
     float ru[3];
@@ -1307,7 +1376,7 @@ __global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArg
     if (s.xpos[tb][2] < m.term_z) d = 1;
     s.x.e.done = d;
   }
-  if (lane == 21) {
+  if (l == 21) {
     float knee = 0, bodyc = 0;
     for (int k = 0; k < s.ncon; k++) {
       if (!(s.con_dist[k] < 0.0f)) continue;
@@ -1321,13 +1390,13 @@ __global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArg
   }
   SYNC();
   // ---- rewards (rewards.py), one term per lane ----
-  if (lane < PP3_NREWARD) {
+  if (l < PP3_NREWARD) {
     const float inv[4] = {s.xquat[1][0], -s.xquat[1][1], -s.xquat[1][2], -s.xquat[1][3]};
     const float cmd0 = s.st[PP3_S_COMMAND], cmd1 = s.st[PP3_S_COMMAND + 1], cmd2 = s.st[PP3_S_COMMAND + 2];
     const float cn = sqrtf(cmd0 * cmd0 + cmd1 * cmd1 + cmd2 * cmd2);
     const float sig = m.sigma;
     float v = 0;
-    switch (lane) {
+    switch (l) {
       case PP3_REWARD_TRACKING_LIN_VEL: {
         float lv[3];
         b_rotate(lv, s.x.e.xdv[1], inv);
@@ -1382,8 +1451,8 @@ __global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArg
         v *= (cn < m.stand_thr) ? 1.0f : 0.0f;
         break;
       case PP3_REWARD_ABDUCTION_ANGLE:
-        for (int l = 0; l < 4; l++) {
-          const float t = s.qpos[7 + 3 * l + 1] - m.des_abd[l];
+        for (int g = 0; g < 4; g++) {
+          const float t = s.qpos[7 + 3 * g + 1] - m.des_abd[g];
           v += t * t;
         }
         break;
@@ -1408,14 +1477,14 @@ __global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArg
       case PP3_REWARD_KNEE_COLLISION: v = s.x.e.knee; break;
       case PP3_REWARD_BODY_COLLISION: v = s.x.e.bodyc; break;
     }
-    s.x.e.rw[lane] = v * m.scales[lane];
+    s.x.e.rw[l] = v * m.scales[l];
   }
   SYNC();
   // ---- state management (environment.py:448-482) ----
   int stepc = (int)s.st[PP3_S_STEP] + 1;
   const bool resample = stepc > m.resample_step;
   const bool isdone = s.x.e.done != 0;
-  if (lane == 0) {
+  if (own && l == 0) {
     float sum = 0.0f;
     for (int k = 0; k < PP3_NREWARD; k++) sum += s.x.e.rw[k];
     a.reward[env] = fminf(fmaxf(sum * m.dt, 0.0f), 10000.0f);
@@ -1424,27 +1493,28 @@ __global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_step_kernel(StepArg
     a.metrics[(size_t)env * PP3_NMETRIC] =
         sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
   }
-  if (lane < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + lane] = s.x.e.rw[lane];
-  if (lane < NU) {
-    s.st[PP3_S_LAST_ACT + lane] = act_env[lane];
-    s.st[PP3_S_LAST_VEL + lane] = s.qvel[6 + lane];
+  if (own && l < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + l] = s.x.e.rw[l];
+  if (l < NU) {
+    s.st[PP3_S_LAST_ACT + l] = act_env[l];
+    s.st[PP3_S_LAST_VEL + l] = s.qvel[6 + l];
   }
-  if (lane < 4) {
-    if (s.x.e.filt_mm[lane]) s.st[PP3_S_AIR_TIME + lane] = 0.0f;
-    s.st[PP3_S_LAST_CONTACT + lane] = s.x.e.contact[lane] ? 1.0f : 0.0f;
+  if (l < 4) {
+    if (s.x.e.filt_mm[l]) s.st[PP3_S_AIR_TIME + l] = 0.0f;
+    s.st[PP3_S_LAST_CONTACT + l] = s.x.e.contact[l] ? 1.0f : 0.0f;
   }
   if (resample) {
-    sample_command(m, cmd_key, s.st + PP3_S_COMMAND, lane);
-    sample_orientation(m, cmd_key, s.st + PP3_S_DESIRED_Z, lane);
+    sample_command(m, cmd_key, s.st + PP3_S_COMMAND, l, h);
+    sample_orientation(m, cmd_key, s.st + PP3_S_DESIRED_Z, l, h);
   }
   if (isdone || resample) stepc = 0;
-  if (lane == 0) s.st[PP3_S_STEP] = (float)stepc;
-  if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, lane);
+  if (l == 0) s.st[PP3_S_STEP] = (float)stepc;
+  if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
   SYNC();
-  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) gst[i] = s.st[i];
+  if (own)
+    for (int i = l; i < PP3_S_ACT_BUF; i += HW) gst[i] = s.st[i];
   PHASE(12);
 #ifdef PP3_PHASE_PROF
-  if (lane < 13) atomicAdd(&g_prof[lane], (unsigned long long)s.prof[lane]);
+  if (l < 13) atomicAdd(&g_prof[l], (unsigned long long)s.prof[l]);
 #endif
 }
 
@@ -1463,59 +1533,65 @@ struct ResetArgs {
 };
 
 template <int NC>
-__global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void env_reset_kernel(ResetArgs a) {
-  __shared__ Shared<NC> s;
-  const int env = blockIdx.x;
+__global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
+  __shared__ Shared<NC> sh[2];
   const int lane = threadIdx.x;
-  if (env >= a.N) return;
-  if (a.mask && !a.mask[env]) return;
+  const int h = lane >> 5, l = lane & (HW - 1);
+  const int env_raw = 2 * blockIdx.x + h;
+  const int env = env_raw < a.N ? env_raw : a.N - 1;
+  // envs outside N or masked out compute alongside their wave partner but store nothing
+  const bool own = env_raw < a.N && (!a.mask || a.mask[env]);
+  Shared<NC>& s = sh[h];
   const DevModel& m = *a.m;
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * m.stride;
-  load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, lane);
-  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) s.st[i] = 0.0f;
-  for (int i = PP3_S_ACT_BUF + lane; i < m.stride; i += WAVE) gst[i] = 0.0f;  // latency buffers
+  load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
+  for (int i = l; i < PP3_S_ACT_BUF; i += HW) s.st[i] = 0.0f;
+  if (own)
+    for (int i = PP3_S_ACT_BUF + l; i < m.stride; i += HW) gst[i] = 0.0f;  // latency buffers
   SYNC();
   const Key rng{a.keys[2 * env], a.keys[2 * env + 1]};
-  const Key kl = split_i(rng, 4, lane < 4 ? lane : 0, part);
-  const Key k0 = bcast_key(kl, 0), kcmd = bcast_key(kl, 1), kori = bcast_key(kl, 2), kpos = bcast_key(kl, 3);
+  const Key kl = split_i(rng, 4, l < 4 ? l : 0, part);
+  const Key k0 = hkey(kl, 0, h), kcmd = hkey(kl, 1, h), kori = hkey(kl, 2, h), kpos = hkey(kl, 3, h);
   // randomize_qpos (domain_randomization.py:188-210) on the home keyframe with default_pose
   float u = 0;
-  if (lane < 4) {
-    const Key kk = split_i(kpos, 3, lane < 3 ? 1 : 2, part);
-    u = lane < 3 ? uniform_i(kk, 3, lane, m.start_lo[lane], m.start_hi[lane], part)
-                 : uniform_i(kk, 1, 0, -m.pi_f, m.pi_f, part);
+  if (l < 4) {
+    const Key kk = split_i(kpos, 3, l < 3 ? 1 : 2, part);
+    u = l < 3 ? uniform_i(kk, 3, l, m.start_lo[l], m.start_hi[l], part)
+              : uniform_i(kk, 1, 0, -m.pi_f, m.pi_f, part);
   }
-  const float yaw = rlane(u, 3);
-  if (lane < NQ) {
-    float q = lane >= 7 ? m.default_pose[lane - 7] : m.key_qpos[lane];
-    if (lane < 3) q = u;
-    if (lane == 3) q = cosf(yaw / 2.0f);
-    if (lane == 4 || lane == 5) q = 0.0f;
-    if (lane == 6) q = sinf(yaw / 2.0f);
-    s.qpos[lane] = q;
+  const float yaw = hb(u, 3, h);
+  if (l < NQ) {
+    float q = l >= 7 ? m.default_pose[l - 7] : m.key_qpos[l];
+    if (l < 3) q = u;
+    if (l == 3) q = cosf(yaw / 2.0f);
+    if (l == 4 || l == 5) q = 0.0f;
+    if (l == 6) q = sinf(yaw / 2.0f);
+    s.qpos[l] = q;
   }
-  if (lane < NV) { s.qvel[lane] = 0.0f; s.qws[lane] = 0.0f; }
-  if (lane < NU) s.ctrl[lane] = 0.0f;
+  if (l < NV) { s.qvel[l] = 0.0f; s.qws[l] = 0.0f; }
+  if (l < NU) s.ctrl[l] = 0.0f;
   SYNC();
-  substep(s, m, lane, false);  // pipeline_init: mjx.forward at (q, qd=0, ctrl=0)
-  if (lane < NQ) s.st[PP3_S_QPOS + lane] = s.qpos[lane];
-  if (lane < NV) { s.st[PP3_S_QVEL + lane] = 0.0f; s.st[PP3_S_QACC_WS + lane] = s.qws[lane]; }
-  if (lane == 0) {
+  substep(s, m, l, h, false);  // pipeline_init: mjx.forward at (q, qd=0, ctrl=0)
+  if (l < NQ) s.st[PP3_S_QPOS + l] = s.qpos[l];
+  if (l < NV) { s.st[PP3_S_QVEL + l] = 0.0f; s.st[PP3_S_QACC_WS + l] = s.qws[l]; }
+  if (l == 0) {
     s.st[PP3_S_RNG] = __uint_as_float(k0.a);
     s.st[PP3_S_RNG + 1] = __uint_as_float(k0.b);
   }
-  sample_command(m, kcmd, s.st + PP3_S_COMMAND, lane);
-  sample_orientation(m, kori, s.st + PP3_S_DESIRED_Z, lane);
-  if (lane < m.Li) gst[m.imu_off + 5 * m.Li + lane] = -1.0f;  // initial_imu_buffer gravity row
+  sample_command(m, kcmd, s.st + PP3_S_COMMAND, l, h);
+  sample_orientation(m, kori, s.st + PP3_S_DESIRED_Z, l, h);
+  if (own && l < m.Li) gst[m.imu_off + 5 * m.Li + l] = -1.0f;  // initial_imu_buffer gravity row
+  __threadfence_block();
   SYNC();
-  get_obs(s, m, gst + m.imu_off, lane);
-  write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, lane);
-  if (lane == 0) { a.reward[env] = 0.0f; a.done[env] = 0.0f; }
-  if (lane < PP3_NMETRIC) a.metrics[(size_t)env * PP3_NMETRIC + lane] = 0.0f;
-  if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, lane);
+  get_obs(s, m, gst + m.imu_off, l, h, own);
+  write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, l, own);
+  if (own && l == 0) { a.reward[env] = 0.0f; a.done[env] = 0.0f; }
+  if (own && l < PP3_NMETRIC) a.metrics[(size_t)env * PP3_NMETRIC + l] = 0.0f;
+  if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
   SYNC();
-  for (int i = lane; i < PP3_S_ACT_BUF; i += WAVE) gst[i] = s.st[i];
+  if (own)
+    for (int i = l; i < PP3_S_ACT_BUF; i += HW) gst[i] = s.st[i];
 }
 
 struct PhysArgs {
@@ -1529,29 +1605,30 @@ struct PhysArgs {
 };
 
 template <int NC>
-__global__ __launch_bounds__(WAVE, NC == 8 ? 4 : 3) void physics_kernel(PhysArgs a) {
-  __shared__ Shared<NC> s;
-  const int env = blockIdx.x;
+__global__ __launch_bounds__(WAVE, 2) void physics_kernel(PhysArgs a) {
+  __shared__ Shared<NC> sh[2];
   const int lane = threadIdx.x;
-  if (env >= a.N) return;
+  const int h = lane >> 5, l = lane & (HW - 1);
+  const int env_raw = 2 * blockIdx.x + h;
+  const bool own = env_raw < a.N;
+  const int env = own ? env_raw : a.N - 1;
+  Shared<NC>& s = sh[h];
   const DevModel& m = *a.m;
   float* gst = a.state + (size_t)env * m.stride;
-  load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, lane);
-  if (lane < NQ) s.qpos[lane] = gst[PP3_S_QPOS + lane];
-  if (lane < NV) { s.qvel[lane] = gst[PP3_S_QVEL + lane]; s.qws[lane] = gst[PP3_S_QACC_WS + lane]; }
-  if (lane < NU) s.ctrl[lane] = a.ctrl[(size_t)env * NU + lane];
+  load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
+  if (l < NQ) s.qpos[l] = gst[PP3_S_QPOS + l];
+  if (l < NV) { s.qvel[l] = gst[PP3_S_QVEL + l]; s.qws[l] = gst[PP3_S_QACC_WS + l]; }
+  if (l < NU) s.ctrl[l] = a.ctrl[(size_t)env * NU + l];
   SYNC();
   for (int i = 0; i < a.nsteps; i++) {
     const DevModel* mp = a.m;
-    int ln = lane;
-    // opaque per iteration: keep model loads and lane-derived addresses inside the substep
-    // (hoisting them out of the loop costs more registers than recomputing them)
-    asm volatile("" : "+s"(mp), "+v"(ln));
-    substep(s, *mp, ln, true);
+    asm volatile("" : "+s"(mp));
+    substep(s, *mp, l, h, true);
   }
-  if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, lane);
-  if (lane < NQ) gst[PP3_S_QPOS + lane] = s.qpos[lane];
-  if (lane < NV) { gst[PP3_S_QVEL + lane] = s.qvel[lane]; gst[PP3_S_QACC_WS + lane] = s.qws[lane]; }
+  if (!own) return;
+  if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
+  if (l < NQ) gst[PP3_S_QPOS + l] = s.qpos[l];
+  if (l < NV) { gst[PP3_S_QVEL + l] = s.qvel[l]; gst[PP3_S_QACC_WS + l] = s.qws[l]; }
 }
 
 __global__ void fill_uniform_kernel(float* p, int64_t n, uint32_t seed, uint32_t ctr, float lo, float hi) {
@@ -1980,8 +2057,8 @@ int pp3_reset(pp3_env_t* e, const uint32_t* keys_dev, const uint8_t* mask_dev, v
   a.dr = e->dr_on ? e->dr : nullptr;
   a.pipe = e->pipe_on ? e->pipe : nullptr;
   a.N = e->N;
-  if (e->nc == 8) hipLaunchKernelGGL(env_reset_kernel<8>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
-  else hipLaunchKernelGGL(env_reset_kernel<16>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  if (e->nc == 8) hipLaunchKernelGGL(env_reset_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
+  else hipLaunchKernelGGL(env_reset_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
   return PP3_OK;
 }
@@ -2001,8 +2078,8 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   a.dr = e->dr_on ? e->dr : nullptr;
   a.pipe = e->pipe_on ? e->pipe : nullptr;
   a.N = e->N;
-  if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
-  else hipLaunchKernelGGL(env_step_kernel<16>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
+  else hipLaunchKernelGGL(env_step_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
   e->obs_cur ^= 1;
   return PP3_OK;
@@ -2034,8 +2111,8 @@ int pp3_physics_step(pp3_env_t* e, const float* ctrl_dev, int32_t nsteps, void* 
   a.pipe = e->pipe;
   a.nsteps = nsteps;
   a.N = e->N;
-  if (e->nc == 8) hipLaunchKernelGGL(physics_kernel<8>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
-  else hipLaunchKernelGGL(physics_kernel<16>, dim3(e->N), dim3(WAVE), 0, stream_of(e, stream), a);
+  if (e->nc == 8) hipLaunchKernelGGL(physics_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
+  else hipLaunchKernelGGL(physics_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
   return PP3_OK;
 }
@@ -2124,6 +2201,12 @@ int pp3_fill_uniform(pp3_env_t* e, float* dev, int64_t count, uint32_t seed, uin
   return PP3_OK;
 }
 
+#ifdef PP3_DEBUG
+extern "C" int pp3_debug_read(float* out) {
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(float) * 512));
+  return PP3_OK;
+}
+#endif
 int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset) {
 #ifdef PP3_PHASE_PROF
   if (n > NPROF) n = NPROF;

@@ -49,3 +49,29 @@ def oracle_state_to_record(st: np.ndarray) -> np.ndarray:
     out = st.astype(np.float32)
     out[..., _abi.S_RNG:_abi.S_RNG + 2] = st[..., _abi.S_RNG:_abi.S_RNG + 2].astype(np.uint32).view(np.float32)
     return out
+
+
+class FlipBudget:
+    """Env-step parity with an explicit allowance for constraint-state flips.
+
+    MuJoCo's Newton solver (iterations=1) is discontinuous where a constraint row sits on its
+    switch point (satisfied/active, or the frictionloss kink): the fp32 kernel and the oracle
+    may then take different branches and legitimately produce different accelerations.  A
+    step may exceed the tolerance only if the oracle flagged such a row during that step
+    (OracleEnv.step()['boundary'] > 0), and at most `max_frac` of all compared steps may.
+    """
+
+    def __init__(self, max_frac=0.05):
+        self.max_frac = max_frac
+        self.n = 0
+        self.flips = 0
+
+    def check(self, ok: bool, oracle_out: dict, what: str = ""):
+        self.n += 1
+        if ok:
+            return
+        assert oracle_out.get("boundary", 0) > 0, f"parity failure without a constraint-state flip: {what}"
+        self.flips += 1
+
+    def finish(self):
+        assert self.flips <= max(1, self.max_frac * self.n), (self.flips, self.n)
