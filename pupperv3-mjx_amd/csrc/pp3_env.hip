@@ -95,7 +95,11 @@ struct alignas(16) Shared {
 #endif
 };
 
-#define SYNC() __syncthreads()
+// A workgroup is ONE wave and LDS executes a wave's instructions in issue order, so a lane's
+// LDS store is visible to every later LDS load of the same wave: phase boundaries only need to
+// stop the compiler from reordering LDS accesses across them.  (__syncthreads would also
+// drain outstanding global loads, s_waitcnt vmcnt(0), and serialise the LDS queue.)
+#define SYNC() asm volatile("" ::: "memory")
 
 // Diagnostic build only (-DPP3_PHASE_PROF): per-phase s_memtime deltas summed over all envs.
 #ifdef PP3_PHASE_PROF
@@ -129,15 +133,16 @@ __device__ __forceinline__ uint32_t hbu(uint32_t v, int k, int h) {
   return h ? b : a;
 }
 __device__ __forceinline__ Key hkey(Key k, int l, int h) { return Key{hbu(k.a, l, h), hbu(k.b, l, h)}; }
-// sum over the 32 lanes of this lane's half: DPP butterflies inside each 16-lane row,
-// row_bcast:15 folds row 0 into row 1 (and row 2 into row 3); lanes 31 / 63 hold the totals
-__device__ __forceinline__ float hsum(float v, int h) {
+// sum over the 32 lanes of this lane's half, left in every lane: DPP butterflies give each
+// 16-lane row its sum, then v_permlane16_swap (gfx950) pairs row 0 with row 1 and row 2 with
+// row 3.  No SGPR round trip, so no readlane hazard stalls.
+__device__ __forceinline__ float hsum(float v, int) {
   v += dpp_f<0xB1, 0xF>(v, 0.0f);   // quad_perm [1,0,3,2]
   v += dpp_f<0x4E, 0xF>(v, 0.0f);   // quad_perm [2,3,0,1]
   v += dpp_f<0x141, 0xF>(v, 0.0f);  // row_half_mirror
   v += dpp_f<0x140, 0xF>(v, 0.0f);  // row_mirror
-  v += dpp_f<0x142, 0xA>(v, 0.0f);  // row_bcast:15 -> rows 1, 3
-  return hb(v, HW - 1, h);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 // this half's bits of a ballot
 __device__ __forceinline__ uint32_t hballot(bool p, int h) {
@@ -545,7 +550,7 @@ __device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int l, flo
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     col[slot] = a[k];
-    __syncthreads();
+    SYNC();
     float r[20];
 #pragma unroll
     for (int q = (k & ~3); q < 20; q += 4) {
@@ -558,7 +563,7 @@ __device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int l, flo
 #pragma unroll
     for (int j = k + 1; j < NV; ++j) a[j] -= lik * r[j];
     a[k] = (l > k) ? lik : a[k];
-    __syncthreads();  // col is rewritten by the next pivot
+    SYNC();  // col is rewritten by the next pivot
   }
 }
 // solve L D L^T x = b; x = b_i on entry (lane i).  Uses s.x.L for the transposed factor.
@@ -1583,7 +1588,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   sample_orientation(m, kori, s.st + PP3_S_DESIRED_Z, l, h);
   if (own && l < m.Li) gst[m.imu_off + 5 * m.Li + l] = -1.0f;  // initial_imu_buffer gravity row
   __threadfence_block();
-  SYNC();
+  __syncthreads();  // the gravity row above is global memory written by other lanes
   get_obs(s, m, gst + m.imu_off, l, h, own);
   write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, l, own);
   if (own && l == 0) { a.reward[env] = 0.0f; a.done[env] = 0.0f; }
