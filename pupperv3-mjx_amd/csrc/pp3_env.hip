@@ -28,6 +28,7 @@
 namespace pp3 {
 
 constexpr int HW = 32;      // lanes per environment (half wave)
+typedef __attribute__((address_space(4))) const DevModel GModel;  // DevModel: read-only (constant AS)
 constexpr int HMAX = 16;    // observation_history limit
 constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + HW - 1) / HW;
 constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
@@ -335,9 +336,15 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, i
   const float margin = m.pair_margin[p];
   float p1[3], p2[3];
   const int s1 = m.cg_slot[g1], s2 = m.cg_slot[g2];
-  for (int k = 0; k < 3; k++) {
-    p1[k] = s1 >= 0 ? s.gxpos[s1][k] : m.cg_pos[g1][k];
-    p2[k] = s2 >= 0 ? s.gxpos[s2][k] : m.cg_pos[g2][k];
+  {  // robot geoms: world position from LDS; static geoms: from the model (separate loads so
+     // the select is on values, not on an LDS/global pointer, which would become a flat load)
+    const int i1 = s1 >= 0 ? s1 : 0, i2 = s2 >= 0 ? s2 : 0;
+    float l1[3], l2[3], c1[3], c2[3];
+    for (int k = 0; k < 3; k++) {
+      l1[k] = s.gxpos[i1][k]; l2[k] = s.gxpos[i2][k];
+      c1[k] = m.cg_pos[g1][k]; c2[k] = m.cg_pos[g2][k];
+    }
+    for (int k = 0; k < 3; k++) { p1[k] = s1 >= 0 ? l1[k] : c1[k]; p2[k] = s2 >= 0 ? l2[k] : c2[k]; }
   }
   if (t1 == PP3_GEOM_PLANE && t2 == PP3_GEOM_SPHERE) {
     const float* R1 = m.cg_wmat[g1];
@@ -406,7 +413,8 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const DevModel& m, 
   s.con_dist[slot] = dist;
   for (int k = 0; k < 3; k++) s.x.a.con_pos[slot][k] = pos[k];
   make_frame(s.x.a.con_frame[slot], nrm);
-  s.con_mu[slot] = s.dr_on ? s.fric : m.pair_mu[p];
+  const float mu_dr = s.fric, mu_model = m.pair_mu[p];  // values, not a pointer select (flat load)
+  s.con_mu[slot] = s.dr_on ? mu_dr : mu_model;
 }
 
 // Phase 3a: collision (mj_collision), contacts compacted in pair order; when more than
@@ -1338,9 +1346,12 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   PHASE(10);
   // ---- physics: n_frames x mj_step (environment.py:366) ----
   for (int f = 0; f < m.n_frames; f++) {
-    const DevModel* mp = a.m;
-    asm volatile("" : "+s"(mp));  // keep model loads inside the substep (no loop-carried registers)
-    substep(s, *mp, l, h, true);
+    // opaque per iteration: keep model loads inside the substep (hoisting them costs more
+    // registers than reloading them); the constant address space is restated after the asm so
+    // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
+    const GModel* mp = (const GModel*)(a.m);
+    asm volatile("" : "+s"(mp));
+    substep(s, *(const DevModel*)mp, l, h, true);
   }
   if (l < NQ) s.st[PP3_S_QPOS + l] = s.qpos[l];
   if (l < NV) { s.st[PP3_S_QVEL + l] = s.qvel[l]; s.st[PP3_S_QACC_WS + l] = s.qws[l]; }
@@ -1626,9 +1637,9 @@ __global__ __launch_bounds__(WAVE, 2) void physics_kernel(PhysArgs a) {
   if (l < NU) s.ctrl[l] = a.ctrl[(size_t)env * NU + l];
   SYNC();
   for (int i = 0; i < a.nsteps; i++) {
-    const DevModel* mp = a.m;
+    const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    substep(s, *mp, l, h, true);
+    substep(s, *(const DevModel*)mp, l, h, true);
   }
   if (!own) return;
   if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
