@@ -1360,7 +1360,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   get_obs(s, m, gst + m.imu_off, l, h, own);
   write_obs(s, m, a.obs_in + (size_t)env * PP3_OBS_DIM * m.H, a.obs_out + (size_t)env * PP3_OBS_DIM * m.H, l, own);
   PHASE(11);
-  // ---- brax x/xd, feet, done, collisions ----
+  // ---- brax x/xd (lanes 1..13), feet (16..19) ----
   if (l >= 1 && l < NB) {
     const int b = l;
     const float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]};
@@ -1379,137 +1379,110 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     s.x.e.first[f] = (s.st[PP3_S_AIR_TIME + f] > 0.0f && (c | last)) ? 1.0f : 0.0f;
     s.st[PP3_S_AIR_TIME + f] += m.dt;
   }
-  if (l == 20) {
-    const int tb = m.torso_body;
-    const float up[3] = {0, 0, 1};
-    float ru[3];
-    b_rotate(ru, up, s.xquat[tb]);
-    int d = dot3(ru, up) < m.cos_term_angle;
-    for (int j = 0; j < 12; j++) {
-      if (s.qpos[7 + j] < m.jlo[j]) d = 1;
-      if (s.qpos[7 + j] > m.jhi[j]) d = 1;
-    }
-    if (s.xpos[tb][2] < m.term_z) d = 1;
-    s.x.e.done = d;
-  }
-  if (l == 21) {
-    float knee = 0, bodyc = 0;
-    for (int k = 0; k < s.ncon; k++) {
-      if (!(s.con_dist[k] < 0.0f)) continue;
-      const int pp = s.con_pair[k];
-      const int ga = m.cg_id[m.pair_g1[pp]], gb = m.cg_id[m.pair_g2[pp]];
-      for (int i = 0; i < m.n_knee_geoms; i++) knee += (ga == m.knee_geoms[i] || gb == m.knee_geoms[i]) ? 1.0f : 0.0f;
-      for (int i = 0; i < m.n_torso_geoms; i++) bodyc += (ga == m.torso_geoms[i] || gb == m.torso_geoms[i]) ? 1.0f : 0.0f;
-    }
-    s.x.e.knee = knee;
-    s.x.e.bodyc = bodyc;
-  }
   SYNC();
-  // ---- rewards (rewards.py), one term per lane ----
-  if (l < PP3_NREWARD) {
+  // ---- done (environment.py:383-388): tilt and height on every lane, joint limits on 0..11 ----
+  const int tb = m.torso_body;
+  const float z0[3] = {0, 0, 1};
+  float ru_t[3];
+  b_rotate(ru_t, z0, s.xquat[tb]);
+  const bool jviol = l < 12 && (s.qpos[7 + l] < m.jlo[l] || s.qpos[7 + l] > m.jhi[l]);
+  const bool isdone = hballot(jviol, h) != 0 || ru_t[2] < m.cos_term_angle || s.xpos[tb][2] < m.term_z;
+  // ---- rewards (rewards.py) ----
+  // sums over joints / dofs / feet / contacts: one element per lane, then a half-wave sum
+  const float cmd0 = s.st[PP3_S_COMMAND], cmd1 = s.st[PP3_S_COMMAND + 1], cmd2 = s.st[PP3_S_COMMAND + 2];
+  const float cn = sqrtf(cmd0 * cmd0 + cmd1 * cmd1 + cmd2 * cmd2);
+  float r_torq = 0, r_jacc = 0, r_mech = 0, r_arate = 0, r_stand = 0, r_standv = 0, r_abd = 0;
+  float r_air = 0, r_slip = 0, r_knee = 0, r_body = 0;
+  if (l < NV) r_torq = s.qfrc_act[l] * s.qfrc_act[l];
+  if (l < 12) {
+    const float qv = s.qvel[6 + l], qp = s.qpos[7 + l];
+    const float acc = (qv - s.st[PP3_S_LAST_VEL + l]) / m.env_dt;
+    r_jacc = acc * acc;
+    r_mech = fabsf(s.qfrc_act[6 + l] * qv);
+    const float da = act_env[l] - s.st[PP3_S_LAST_ACT + l];
+    r_arate = da * da;
+    r_stand = fabsf(qp - m.default_pose[l]);
+    r_standv = fabsf(qv);
+    if (l % 3 == 1) { const float t = qp - m.des_abd[l / 3]; r_abd = t * t; }
+  }
+  if (l < 4) {
+    r_air = (s.st[PP3_S_AIR_TIME + l] - 0.1f) * s.x.e.first[l];
+    const int b = m.lower_leg_body[l];
+    const float* sp = s.foot_xpos[l];
+    const float off[3] = {sp[0] - s.xpos[b][0], sp[1] - s.xpos[b][1], sp[2] - s.xpos[b][2]};
+    float cr[3];
+    cross3(cr, s.x.e.xda[b], off);
+    const float vx = s.x.e.xdv[b][0] + cr[0], vy = s.x.e.xdv[b][1] + cr[1];
+    r_slip = (vx * vx + vy * vy) * (s.x.e.filt_cm[l] ? 1.0f : 0.0f);
+  }
+  if (l < s.ncon && s.con_dist[l] < 0.0f) {  // geom_collision: (contact, id) matches with dist < 0
+    const int pp = s.con_pair[l];
+    const int ga = m.cg_id[m.pair_g1[pp]], gb = m.cg_id[m.pair_g2[pp]];
+    for (int i = 0; i < m.n_knee_geoms; i++) r_knee += (ga == m.knee_geoms[i] || gb == m.knee_geoms[i]) ? 1.0f : 0.0f;
+    for (int i = 0; i < m.n_torso_geoms; i++) r_body += (ga == m.torso_geoms[i] || gb == m.torso_geoms[i]) ? 1.0f : 0.0f;
+  }
+  r_torq = hsum(r_torq, h);
+  r_jacc = hsum(r_jacc, h);
+  r_mech = hsum(r_mech, h);
+  r_arate = hsum(r_arate, h);
+  r_stand = hsum(r_stand, h) * ((cn < 0.1f) ? 1.0f : 0.0f);
+  r_standv = hsum(r_standv, h) * ((cn < m.stand_thr) ? 1.0f : 0.0f);
+  r_abd = hsum(r_abd, h);
+  r_air = hsum(r_air, h) * ((cn > 0.05f) ? 1.0f : 0.0f);
+  r_slip = hsum(r_slip, h);
+  r_knee = hsum(r_knee, h);
+  r_body = hsum(r_body, h);
+  // single-valued terms: straight-line code on every lane (no divergent switch)
+  float rw[PP3_NREWARD];
+  {
     const float inv[4] = {s.xquat[1][0], -s.xquat[1][1], -s.xquat[1][2], -s.xquat[1][3]};
-    const float cmd0 = s.st[PP3_S_COMMAND], cmd1 = s.st[PP3_S_COMMAND + 1], cmd2 = s.st[PP3_S_COMMAND + 2];
-    const float cn = sqrtf(cmd0 * cmd0 + cmd1 * cmd1 + cmd2 * cmd2);
     const float sig = m.sigma;
-    float v = 0;
-    switch (l) {
-      case PP3_REWARD_TRACKING_LIN_VEL: {
-        float lv[3];
-        b_rotate(lv, s.x.e.xdv[1], inv);
-        const float e = (cmd0 - lv[0]) * (cmd0 - lv[0]) + (cmd1 - lv[1]) * (cmd1 - lv[1]);
-        v = expf(-e / sig);
-      } break;
-      case PP3_REWARD_TRACKING_ANG_VEL: {
-        float av[3];
-        b_rotate(av, s.x.e.xda[1], inv);
-        v = expf(-(cmd2 - av[2]) * (cmd2 - av[2]) / sig);
-      } break;
-      case PP3_REWARD_TRACKING_ORIENTATION: {
-        const float z0[3] = {0, 0, 1};
-        float wz[3];
-        b_rotate(wz, z0, inv);
-        float e = 0;
-        for (int k = 0; k < 3; k++) e += (wz[k] - s.st[PP3_S_DESIRED_Z + k]) * (wz[k] - s.st[PP3_S_DESIRED_Z + k]);
-        v = expf(-e / sig);
-      } break;
-      case PP3_REWARD_LIN_VEL_Z: v = s.x.e.xdv[1][2] * s.x.e.xdv[1][2]; break;
-      case PP3_REWARD_ANG_VEL_XY: v = s.x.e.xda[1][0] * s.x.e.xda[1][0] + s.x.e.xda[1][1] * s.x.e.xda[1][1]; break;
-      case PP3_REWARD_ORIENTATION: {
-        const float z0[3] = {0, 0, 1};
-        float ru[3];
-        b_rotate(ru, z0, s.xquat[1]);
-        v = ru[0] * ru[0] + ru[1] * ru[1];
-      } break;
-      case PP3_REWARD_TORQUES:
-        for (int i = 0; i < NV; i++) v += s.qfrc_act[i] * s.qfrc_act[i];
-        break;
-      case PP3_REWARD_JOINT_ACCELERATION:
-        for (int j = 0; j < 12; j++) {
-          const float acc = (s.qvel[6 + j] - s.st[PP3_S_LAST_VEL + j]) / m.env_dt;
-          v += acc * acc;
-        }
-        break;
-      case PP3_REWARD_MECHANICAL_WORK:
-        for (int j = 0; j < 12; j++) v += fabsf(s.qfrc_act[6 + j] * s.qvel[6 + j]);
-        break;
-      case PP3_REWARD_ACTION_RATE:
-        for (int j = 0; j < 12; j++) {
-          const float d = act_env[j] - s.st[PP3_S_LAST_ACT + j];
-          v += d * d;
-        }
-        break;
-      case PP3_REWARD_STAND_STILL:
-        for (int j = 0; j < 12; j++) v += fabsf(s.qpos[7 + j] - m.default_pose[j]);
-        v *= (cn < 0.1f) ? 1.0f : 0.0f;
-        break;
-      case PP3_REWARD_STAND_STILL_JOINT_VELOCITY:
-        for (int j = 0; j < 12; j++) v += fabsf(s.qvel[6 + j]);
-        v *= (cn < m.stand_thr) ? 1.0f : 0.0f;
-        break;
-      case PP3_REWARD_ABDUCTION_ANGLE:
-        for (int g = 0; g < 4; g++) {
-          const float t = s.qpos[7 + 3 * g + 1] - m.des_abd[g];
-          v += t * t;
-        }
-        break;
-      case PP3_REWARD_FEET_AIR_TIME:
-        for (int f = 0; f < 4; f++) v += (s.st[PP3_S_AIR_TIME + f] - 0.1f) * s.x.e.first[f];
-        v *= (cn > 0.05f) ? 1.0f : 0.0f;
-        break;
-      case PP3_REWARD_FOOT_SLIP:
-        for (int f = 0; f < 4; f++) {
-          const int b = m.lower_leg_body[f];
-          const float* sp = s.foot_xpos[f];
-          const float off[3] = {sp[0] - s.xpos[b][0], sp[1] - s.xpos[b][1], sp[2] - s.xpos[b][2]};
-          float cr[3];
-          cross3(cr, s.x.e.xda[b], off);
-          const float vx = s.x.e.xdv[b][0] + cr[0], vy = s.x.e.xdv[b][1] + cr[1];
-          v += (vx * vx + vy * vy) * (s.x.e.filt_cm[f] ? 1.0f : 0.0f);
-        }
-        break;
-      case PP3_REWARD_TERMINATION:
-        v = (s.x.e.done && (int)s.st[PP3_S_STEP] < m.term_step) ? 1.0f : 0.0f;
-        break;
-      case PP3_REWARD_KNEE_COLLISION: v = s.x.e.knee; break;
-      case PP3_REWARD_BODY_COLLISION: v = s.x.e.bodyc; break;
-    }
-    s.x.e.rw[l] = v * m.scales[l];
+    const float* xdv1 = s.x.e.xdv[1];
+    const float* xda1 = s.x.e.xda[1];
+    float lv[3], av[3], wz[3], ru[3];
+    b_rotate(lv, xdv1, inv);
+    b_rotate(av, xda1, inv);
+    b_rotate(wz, z0, inv);
+    b_rotate(ru, z0, s.xquat[1]);
+    const float e_lin = (cmd0 - lv[0]) * (cmd0 - lv[0]) + (cmd1 - lv[1]) * (cmd1 - lv[1]);
+    float e_ori = 0;
+    for (int k = 0; k < 3; k++) e_ori += (wz[k] - s.st[PP3_S_DESIRED_Z + k]) * (wz[k] - s.st[PP3_S_DESIRED_Z + k]);
+    rw[PP3_REWARD_TRACKING_LIN_VEL] = expf(-e_lin / sig);
+    rw[PP3_REWARD_TRACKING_ANG_VEL] = expf(-(cmd2 - av[2]) * (cmd2 - av[2]) / sig);
+    rw[PP3_REWARD_TRACKING_ORIENTATION] = expf(-e_ori / sig);
+    rw[PP3_REWARD_LIN_VEL_Z] = xdv1[2] * xdv1[2];
+    rw[PP3_REWARD_ANG_VEL_XY] = xda1[0] * xda1[0] + xda1[1] * xda1[1];
+    rw[PP3_REWARD_ORIENTATION] = ru[0] * ru[0] + ru[1] * ru[1];
   }
-  SYNC();
+  rw[PP3_REWARD_TORQUES] = r_torq;
+  rw[PP3_REWARD_JOINT_ACCELERATION] = r_jacc;
+  rw[PP3_REWARD_MECHANICAL_WORK] = r_mech;
+  rw[PP3_REWARD_ACTION_RATE] = r_arate;
+  rw[PP3_REWARD_STAND_STILL] = r_stand;
+  rw[PP3_REWARD_STAND_STILL_JOINT_VELOCITY] = r_standv;
+  rw[PP3_REWARD_ABDUCTION_ANGLE] = r_abd;
+  rw[PP3_REWARD_FEET_AIR_TIME] = r_air;
+  rw[PP3_REWARD_FOOT_SLIP] = r_slip;
+  rw[PP3_REWARD_TERMINATION] = (isdone && (int)s.st[PP3_S_STEP] < m.term_step) ? 1.0f : 0.0f;
+  rw[PP3_REWARD_KNEE_COLLISION] = r_knee;
+  rw[PP3_REWARD_BODY_COLLISION] = r_body;
+  float rsum = 0.0f, rmine = 0.0f;  // reward = clip(sum_k scale_k * term_k * dt) in dict order (:446)
+#pragma unroll
+  for (int k = 0; k < PP3_NREWARD; k++) {
+    const float v = rw[k] * m.scales[k];
+    rsum += v;
+    rmine = (l == k) ? v : rmine;
+  }
   // ---- state management (environment.py:448-482) ----
   int stepc = (int)s.st[PP3_S_STEP] + 1;
   const bool resample = stepc > m.resample_step;
-  const bool isdone = s.x.e.done != 0;
   if (own && l == 0) {
-    float sum = 0.0f;
-    for (int k = 0; k < PP3_NREWARD; k++) sum += s.x.e.rw[k];
-    a.reward[env] = fminf(fmaxf(sum * m.dt, 0.0f), 10000.0f);
+    a.reward[env] = fminf(fmaxf(rsum * m.dt, 0.0f), 10000.0f);
     a.done[env] = isdone ? 1.0f : 0.0f;
-    const int tb = m.torso_body;
     a.metrics[(size_t)env * PP3_NMETRIC] =
         sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
   }
-  if (own && l < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + l] = s.x.e.rw[l];
+  if (own && l < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + l] = rmine;
   if (l < NU) {
     s.st[PP3_S_LAST_ACT + l] = act_env[l];
     s.st[PP3_S_LAST_VEL + l] = s.qvel[6 + l];
