@@ -91,7 +91,7 @@ struct alignas(16) Shared {
   float efc_D[NEFC], efc_R[NEFC], efc_aref[NEFC], efc_force[NEFC];
   Scratch<NC> x;
 #ifdef PP3_PHASE_PROF
-  uint64_t prof[16];
+  uint64_t prof[20];
   uint64_t prof_t;
 #endif
 };
@@ -104,7 +104,7 @@ struct alignas(16) Shared {
 
 // Diagnostic build only (-DPP3_PHASE_PROF): per-phase s_memtime deltas summed over all envs.
 #ifdef PP3_PHASE_PROF
-constexpr int NPROF = 16;
+constexpr int NPROF = 20;
 __device__ unsigned long long g_prof[NPROF];
 #define PHASE(k)                                                          \
   do {                                                                    \
@@ -599,6 +599,139 @@ __device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], 
   return x;  // callers SYNC before s.x is rewritten
 }
 
+// ------------------------------------------------------------------------------------
+// Tree-sparse (arrowhead) LDL^T.  In the permuted dof order P = [legs 6..17, base 0..5] the
+// mass matrix and every Hessian whose contacts touch one leg (plus the base) have no
+// leg-leg coupling, so eliminating the legs first creates no fill outside each leg's rows
+// and the base block.  The four legs are independent: pivot level s (0..2) of all four
+// legs is eliminated in ONE round, then the 6 base pivots -- 9 sequential LDS rounds
+// instead of 18, and 99 instead of 153 multiply-adds.  Lane p (< NV) holds permuted row p.
+// ------------------------------------------------------------------------------------
+__host__ __device__ constexpr int pnat(int p) { return p < 12 ? p + 6 : p - 12; }  // permuted -> dof
+__host__ __device__ constexpr int npos(int d) { return d < 6 ? d + 12 : d - 6; }   // dof -> permuted
+
+__device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, float* col /* >= 80 floats */) {
+  const int slot = l < NV ? l : NV;
+#pragma unroll
+  for (int st = 0; st < 3; st++) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) col[20 * g + slot] = a[3 * g + st];
+    SYNC();
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const int k = 3 * g + st;
+      const float* c = col + 20 * g;
+      float r[20];
+#pragma unroll
+      for (int q = (k & ~3); q < 3 * g + 3; q += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(c + q);
+        r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+      }
+#pragma unroll
+      for (int q = 12; q < 20; q += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(c + q);
+        r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+      }
+      const float ik = frcp(fmaxf(r[k], MINVAL));
+      dinv = (l == k) ? ik : dinv;
+      const float lik = a[k] * ik;  // zero on lanes of the other legs
+#pragma unroll
+      for (int j = k + 1; j < 3 * g + 3; ++j) a[j] -= lik * r[j];
+#pragma unroll
+      for (int j = 12; j < NV; ++j) a[j] -= lik * r[j];
+      a[k] = (l > k) ? lik : a[k];
+    }
+    SYNC();
+  }
+#pragma unroll
+  for (int k = 12; k < NV; ++k) {  // dense 6x6 base block
+    col[slot] = a[k];
+    SYNC();
+    float r[20];
+#pragma unroll
+    for (int q = (k & ~3); q < 20; q += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(col + q);
+      r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+    }
+    const float ik = frcp(fmaxf(r[k], MINVAL));
+    dinv = (l == k) ? ik : dinv;
+    const float lik = a[k] * ik;
+#pragma unroll
+    for (int j = k + 1; j < NV; ++j) a[j] -= lik * r[j];
+    a[k] = (l > k) ? lik : a[k];
+    SYNC();
+  }
+}
+// solve L D L^T x = b with the arrowhead factor (permuted order; lane p holds b_p on entry)
+template <int NC>
+__device__ __forceinline__ float ldl_solve_arrow(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int l,
+                                                 int h) {
+  const int lp = l < NV ? l : NV - 1;
+  const int leg = lp < 12 ? lp / 3 : 4, li = lp - 3 * (lp < 12 ? leg : 0);  // leg index, level in leg
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    if (k < l && l < NV) s.x.L[l][k] = a[k];
+  // forward L y = b: three leg levels (four legs at once), then the base
+#pragma unroll
+  for (int st = 0; st < 2; st++) {
+    float y[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) y[g] = hb(x, 3 * g + st, h);
+    float t = x;
+#pragma unroll
+    for (int g = 0; g < 4; g++) t -= (l > 3 * g + st) ? a[3 * g + st] * y[g] : 0.0f;
+    x = t;
+  }
+  {
+    float y[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) y[g] = hb(x, 3 * g + 2, h);
+    float t = x;
+#pragma unroll
+    for (int g = 0; g < 4; g++) t -= (l >= 12) ? a[3 * g + 2] * y[g] : 0.0f;
+    x = t;
+  }
+#pragma unroll
+  for (int k = 12; k < NV - 1; ++k) {
+    const float yk = hb(x, k, h);
+    x = (l > k) ? x - a[k] * yk : x;
+  }
+  x = x * dinv;
+  SYNC();
+  // backward L^T x = y: base pivots (all lanes below), then leg levels 2, 1 (own leg only)
+  float colb[NV];
+#pragma unroll
+  for (int k = 12; k < NV; ++k) colb[k] = s.x.L[k][lp];
+  float cl1 = 0, cl2 = 0;  // L[leg row at level 1 / 2][lp] for lanes at lower levels of that leg
+  if (lp < 12) {
+    const int b0 = 3 * leg;
+    cl1 = li < 1 ? s.x.L[b0 + 1][lp] : 0.0f;
+    cl2 = li < 2 ? s.x.L[b0 + 2][lp] : 0.0f;
+  }
+#pragma unroll
+  for (int k = NV - 1; k >= 12; --k) {
+    const float xk = hb(x, k, h);
+    x = (l < k) ? x - colb[k] * xk : x;
+  }
+#pragma unroll
+  for (int st = 2; st > 0; --st) {
+    float xs[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) xs[g] = hb(x, 3 * g + st, h);
+    const float xl = leg == 0 ? xs[0] : leg == 1 ? xs[1] : leg == 2 ? xs[2] : xs[3];
+    const float cv = st == 2 ? cl2 : cl1;
+    x = (lp < 12 && li < st) ? x - cv * xl : x;
+  }
+  return x;  // callers SYNC before s.x is rewritten
+}
+
+// a[npos(j)] += w . J[.][j] over natural columns [J0, J1) (arrowhead Hessian rows)
+template <int J0, int J1>
+__device__ __forceinline__ void hess_acc_p(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
+#pragma unroll
+  for (int j = J0; j < J1; j++) a[npos(j)] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
+}
+
 // J row r dotted with x (LDS vector)
 template <int NC>
 __device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float* x) {
@@ -652,7 +785,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
   crb_times_cdof(s, m, l);
   rne_chain(s, m, l);
+  PHASE(15);
   collision(s, m, l, h);
+  PHASE(16);
   {
     // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
     bool act = false;
@@ -772,15 +907,16 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     s.efc_aref[r] = -m.pair_b[p] * vel - m.pair_k[p] * imp * (dist - m.pair_margin[p]);
   }
   SYNC();
+  PHASE(13);
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
   {
-    const int li = l < NV ? l : NV - 1;
+    const int lp = l < NV ? l : NV - 1, dn = pnat(lp);  // permuted row held by this lane
     float a[NV], dinv = 1.0f;
 #pragma unroll
-    for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
-    ldl_rows(a, dinv, l, &s.x.L[0][0]);
-    const float x = ldl_solve(s, a, dinv, s.qfrc_smooth[li], l, h);
-    if (l < NV) s.qacc_smooth[l] = x;
+    for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
+    ldl_arrow(a, dinv, l, &s.x.L[0][0]);
+    const float x = ldl_solve_arrow(s, a, dinv, s.qfrc_smooth[dn], l, h);
+    if (l < NV) s.qacc_smooth[dn] = x;
   }
   SYNC();
   PHASE(4);
@@ -893,51 +1029,66 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     gauss = hsum(gauss, h);
     SYNC();
     PHASE(6);
-    // Hessian rows H = M + J' D J (registers), LDL^T, search = -H^-1 grad
+    // Hessian rows H = M + J' D J (registers), LDL^T, search = -H^-1 grad.  Contacts that
+    // touch one leg (+ base) keep H arrowhead -> tree-sparse LDL in permuted order; a contact
+    // coupling two legs (either env of the wave) switches the wave to the dense factorisation.
     {
-      const int li = l < NV ? l : NV - 1;
-      float a[NV], dinv = 1.0f;
-#pragma unroll
-      for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
-      const float dD = s.dofD[li];
-#pragma unroll
-      for (int j = 0; j < NV; j++) a[j] += (j == li) ? dD : 0.0f;
+      bool dense = false;
       for (int c = 0; c < cmax; c++) {
-        const bool cv = c < ncon;
-        // J' D J only over the Jacobian's column support (base + one leg for robot-vs-static
-        // contacts); the union over the wave's two envs is a wave-uniform choice
-        const int sup = cv ? s.con_sup[c] : 4;
-        const int sa = __builtin_amdgcn_readlane(sup, 0), sb = __builtin_amdgcn_readlane(sup, HW);
-        if (cv) {
-          const float* G = s.con_G[c];
-          const float jn = s.Jc[c][0][li], j1 = s.Jc[c][1][li], j2 = s.Jc[c][2][li];
-          const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
-          const float w1 = jn * G[1] + j1 * G[3];
-          const float w2 = jn * G[2] + j2 * G[4];
-          if (sa == 5 || sb == 5) {
-            hess_acc<0, NV>(a, s.Jc[c], w0, w1, w2);
-          } else {
-            hess_acc<0, 6>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 0 || sb == 0) hess_acc<6, 9>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 1 || sb == 1) hess_acc<9, 12>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 2 || sb == 2) hess_acc<12, 15>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 3 || sb == 3) hess_acc<15, 18>(a, s.Jc[c], w0, w1, w2);
+        const int sup = c < ncon ? s.con_sup[c] : 4;
+        dense = dense || __builtin_amdgcn_readlane(sup, 0) == 5 || __builtin_amdgcn_readlane(sup, HW) == 5;
+      }
+      if (!dense) {
+        const int lp = l < NV ? l : NV - 1, dn = pnat(lp);
+        float a[NV], dinv = 1.0f;
+#pragma unroll
+        for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
+        const float dD = s.dofD[dn];
+#pragma unroll
+        for (int j = 0; j < NV; j++) a[j] += (j == lp) ? dD : 0.0f;
+        for (int c = 0; c < cmax; c++) {
+          const bool cv = c < ncon;
+          const int sup = cv ? s.con_sup[c] : 4;
+          const int sa = __builtin_amdgcn_readlane(sup, 0), sb = __builtin_amdgcn_readlane(sup, HW);
+          if (cv) {
+            const float* G = s.con_G[c];
+            const float jn = s.Jc[c][0][dn], j1 = s.Jc[c][1][dn], j2 = s.Jc[c][2][dn];
+            const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
+            const float w1 = jn * G[1] + j1 * G[3];
+            const float w2 = jn * G[2] + j2 * G[4];
+            hess_acc_p<0, 6>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 0 || sb == 0) hess_acc_p<6, 9>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 1 || sb == 1) hess_acc_p<9, 12>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 2 || sb == 2) hess_acc_p<12, 15>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 3 || sb == 3) hess_acc_p<15, 18>(a, s.Jc[c], w0, w1, w2);
           }
         }
+        PHASE(14);
+        ldl_arrow(a, dinv, l, &s.x.L[0][0]);
+        const float x = ldl_solve_arrow(s, a, dinv, s.grad[dn], l, h);
+        if (l < NV) s.search[dn] = -x;
+      } else {
+        const int li = l < NV ? l : NV - 1;
+        float a[NV], dinv = 1.0f;
+#pragma unroll
+        for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
+        const float dD = s.dofD[li];
+#pragma unroll
+        for (int j = 0; j < NV; j++) a[j] += (j == li) ? dD : 0.0f;
+        for (int c = 0; c < cmax; c++) {
+          if (c < ncon) {
+            const float* G = s.con_G[c];
+            const float jn = s.Jc[c][0][li], j1 = s.Jc[c][1][li], j2 = s.Jc[c][2][li];
+            const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
+            const float w1 = jn * G[1] + j1 * G[3];
+            const float w2 = jn * G[2] + j2 * G[4];
+            hess_acc<0, NV>(a, s.Jc[c], w0, w1, w2);
+          }
+        }
+        ldl_rows(a, dinv, l, &s.x.L[0][0]);
+        const float x = ldl_solve(s, a, dinv, s.grad[li], l, h);
+        if (l < NV) s.search[l] = -x;
       }
-#ifdef PP3_DEBUG
-      if (blockIdx.x == 0 && h == 0 && l < NV)
-        for (int j = 0; j < NV; j++) g_dbg[64 + NV * l + j] = a[j];
-      if (blockIdx.x == 0 && h == 0 && l >= 12 && l < 20) {
-        g_dbg[400 + l - 12] = s.efc_D[l];
-        g_dbg[430 + l - 12] = jar[0];
-        g_dbg[440 + l - 12] = s.efc_force[l];
-      }
-      if (blockIdx.x == 0 && h == 0 && l < 10) g_dbg[410 + l] = s.con_G[l / 5][l % 5];
-#endif
-      ldl_rows(a, dinv, l, &s.x.L[0][0]);
-      const float x = ldl_solve(s, a, dinv, s.grad[li], l, h);
-      if (l < NV) s.search[l] = -x;
     }
     SYNC();
     PHASE(7);
@@ -1307,7 +1458,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;
 #ifdef PP3_PHASE_PROF
-  if (l < 16) s.prof[l] = 0;
+  if (l < NPROF) s.prof[l] = 0;
   if (l == 0) s.prof_t = __builtin_amdgcn_s_memtime();
 #endif
   for (int i = l; i < PP3_S_ACT_BUF; i += HW) s.st[i] = gst[i];
@@ -1503,7 +1654,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     for (int i = l; i < PP3_S_ACT_BUF; i += HW) gst[i] = s.st[i];
   PHASE(12);
 #ifdef PP3_PHASE_PROF
-  if (l < 13) atomicAdd(&g_prof[l], (unsigned long long)s.prof[l]);
+  if (l < NPROF) atomicAdd(&g_prof[l], (unsigned long long)s.prof[l]);
 #endif
 }
 

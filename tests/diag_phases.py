@@ -17,9 +17,10 @@ import bench  # noqa: E402
 from pupperv3_mjx import MODEL_XML, _abi, _lib  # noqa: E402
 from pupperv3_mjx.environment import PupperV3Env, make_keys  # noqa: E402
 
-NAMES = ["kinematics", "com/cinert/cdof", "crb*cdof+rne+collision+rows", "M+bias+contactJ", "edge rows+LDL(M)",
-         "warmstart", "newton update+grad", "hessian+LDL+solve", "line search", "integrate",
-         "prologue", "obs", "rewards+state"]
+NAMES = ["kinematics", "com/cinert/cdof", "limit/friction rows+actuation", "M+bias+contactJ", "LDL(M)+solve",
+         "warmstart", "newton update+grad", "LDL(H)+solve", "line search", "integrate",
+         "prologue", "obs", "rewards+state", "bias+contact edge rows", "hessian build", "crb*cdof+rne chain",
+         "collision"]
 
 
 def main():
@@ -32,11 +33,11 @@ def main():
     _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, (steps + 5) * E * 12, 1, 0, -1.0, 1.0, None))
     ms = C.c_float()
     _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, 5, C.byref(ms)))
-    buf = (C.c_uint64 * 16)()
-    _lib.check(L.pp3_phase_profile(buf, 16, 1))
+    buf = (C.c_uint64 * 20)()
+    _lib.check(L.pp3_phase_profile(buf, 20, 1))
     _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + 5 * E * 48), E * 12, steps, C.byref(ms)))
-    _lib.check(L.pp3_phase_profile(buf, 16, 1))
-    v = np.array(buf[:13], dtype=np.float64)
+    _lib.check(L.pp3_phase_profile(buf, 20, 1))
+    v = np.array(buf[:len(NAMES)], dtype=np.float64)
     tot = v.sum()
     print(f"E={E}: {ms.value / steps:.3f} ms/step (prof build); cycles per env-step per env: {tot / (E * steps):.0f}")
     for n, x in zip(NAMES, v):
