@@ -115,3 +115,27 @@ def states_on_boxes(model, n, seed=0, z_range=(0.15, 0.175)):
         qpos[i, 2] = rs.uniform(*z_range)
         qvel[i] *= 0.3
     return qpos, qvel, qws, ctrl
+
+
+def states_with_self_contact(model, jnt_range, n, seed=0, z=0.5):
+    """Seeded states (joint angles uniform in their ranges, base at height z) in which at least
+    one contact is between two robot geoms (a sphere-sphere pair of two different legs), found
+    by rejection sampling against the oracle.  These contacts couple two legs in the Jacobian,
+    which takes the kernel's dense (non-arrowhead) Hessian factorisation path."""
+    from oracle import oracle as O
+    static = {int(model.cgeom_id[g]) for g in range(model.ncgeom) if model.cgeom_bodyid[g] == 0}
+    rs = np.random.RandomState(seed)
+    lo, hi = jnt_range[1:, 0], jnt_range[1:, 1]
+    qs = []
+    while len(qs) < n:
+        q = np.zeros(19)
+        q[2], q[3] = z, 1
+        q[7:] = rs.uniform(lo, hi)
+        p = O.mj_step(model, q, np.zeros(18), np.zeros(18), q[7:].copy(), nsteps=1)[3]
+        k = int(p[_abi.P_NCON])
+        g = p[_abi.P_CON_GEOM:_abi.P_CON_GEOM + 2 * k].reshape(k, 2).astype(int)
+        if any(a not in static and b not in static for a, b in g):
+            qs.append(q)
+    qpos = np.array(qs)
+    qvel = rs.normal(scale=0.3, size=(n, 18))
+    return qpos, qvel, np.zeros((n, 18)), qpos[:, 7:].copy()

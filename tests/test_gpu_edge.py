@@ -69,6 +69,23 @@ def test_sphere_box_contact_parity(box_path, nsteps):
         e.close()
 
 
+@pytest.mark.parametrize("z", [0.5, 0.16])
+def test_self_contact_dense_hessian_path(box_path, z):
+    """Leg-leg sphere contacts couple two legs: the Newton Hessian is no longer arrowhead and
+    the kernel must take its dense LDL path (in the air, z=0.5, and near the ground, z=0.16)."""
+    e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=32)
+    try:
+        m = e.sys_model.struct
+        qpos, qvel, qws, ctrl = common.states_with_self_contact(m, e.sys_model.jnt_range, 32, seed=int(z * 100), z=z)
+        for nsteps in (1, 3):
+            gp, op = _physics_compare(e, m, qpos, qvel, qws, ctrl, nsteps)
+            if nsteps == 1:
+                for i in range(32):
+                    assert _contact_set(gp[i]) == _contact_set(op[i]), i
+    finally:
+        e.close()
+
+
 def test_contact_cap_overflow_keeps_deepest(box_path):
     """More penetrating pairs than the cap: the kernel and the oracle keep the same deepest set."""
     e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=64, max_contacts=8)
