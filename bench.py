@@ -207,13 +207,14 @@ def main():
         launch_s = kernel_ms_max / 1e3 / K
         bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr)
         achieved = bpe * E / launch_s / 1e9
-        traffic, valu = None, None
+        traffic, valu, epw = None, None, 1
         tpath = os.path.join(ROOT, "profiles", "traffic_r01.json")
         if os.path.exists(tpath):
             tj = json.load(open(tpath))
             if tj.get("envs") == E and tj.get("dr", False) == args.dr and not args.obstacles:
                 traffic = tj.get("hbm_bytes_per_launch")
                 valu = tj.get("valu_insts_per_wave")
+                epw = tj.get("envs_per_wave", 1)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -239,10 +240,11 @@ def main():
                          "avg_launch_ms": round(launch_s * 1e3, 4)},
         }
         if valu:
-            # The bound that actually binds (DESIGN.md 'Roofline'): VALU issue.  One wave = one env;
-            # a wave64 VALU instruction occupies its SIMD for 4 cycles; 1024 SIMDs at 2.4 GHz.
-            ceil_s = valu * VALU_CYC * E / (N_SIMD * CLOCK_HZ)
-            out["roofline"]["valu_issue"] = {"valu_insts_per_env_step": valu, "ceiling_ms": round(ceil_s * 1e3, 4),
+            # Compute-side bound (DESIGN.md 'Roofline'): VALU issue.  One wave = `epw` envs; a wave64
+            # VALU instruction occupies its SIMD for 4 cycles; 1024 SIMDs at 2.4 GHz.
+            ceil_s = valu * VALU_CYC * (E / epw) / (N_SIMD * CLOCK_HZ)
+            out["roofline"]["valu_issue"] = {"valu_insts_per_wave": valu, "envs_per_wave": epw,
+                                             "ceiling_ms": round(ceil_s * 1e3, 4),
                                              "frac": round(ceil_s / launch_s, 4),
                                              "source": "profiles/traffic_r01.json (rocprofv3 SQ_INSTS_VALU)"}
         if world == 1:

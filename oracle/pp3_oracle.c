@@ -95,8 +95,8 @@ void orc_threefry2x32(uint32_t k0, uint32_t k1, uint32_t x0, uint32_t x1, uint32
 typedef struct { uint32_t k[2]; } key_t2;
 
 static int g_partitionable = 1;
-static double g_dbg[512];
-static int g_boundary = 0;  /* near-switch constraint rows seen since the last orc_boundary_take() */
+static _Thread_local double g_dbg[512];
+static _Thread_local int g_boundary = 0;  /* near-switch constraint rows seen since the last orc_boundary_take() */
 #define BOUNDARY_REL ((real)1e-4)  /* last Newton iteration's intermediates (debugging aid) */
 static int g_ncon_max = 0; /* contact cap shared with the HIP kernel: 0 = auto (8 flat, 16 with boxes) */
 
