@@ -107,6 +107,8 @@ def main():
     ap.add_argument("--dr", action="store_true", help="domain randomisation on (configs[2])")
     ap.add_argument("--obstacles", type=int, default=0, help="obstacles.py boxes (configs[4])")
     ap.add_argument("--gather", action="store_true", help="RCCL all_gather of obs|reward|done per step (configs[3])")
+    ap.add_argument("--auto-reset", type=int, default=0, metavar="EPISODE_LENGTH",
+                    help="on-device EpisodeWrapper+AutoResetWrapper (brax training wrap) with this episode length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
@@ -143,6 +145,8 @@ def main():
         from pupperv3_mjx import domain_randomization as dr, rng
         sysb, _ = dr.domain_randomize(env.sys, rng.split(rng.PRNGKey(1000 + rank), E))
         env.set_domain_randomization(sysb)
+    if args.auto_reset > 0:
+        _lib.check(L.pp3_set_auto_reset(env._h, args.auto_reset))
     keys = sharding.shard_keys(args.seed, E * world, world, rank)  # global env ids, contiguous shards
     st = env.reset(keys)
     rec = st._record.copy()
@@ -233,7 +237,7 @@ def main():
                                        "domain randomisation" if args.dr else "no DR")),
                        "envs_per_gpu": E, "global_envs": E * world, "obs_history": env._observation_history,
                        "n_frames": env._n_frames, "parallelism": f"env-sharded x{world} (no data-path collective)",
-                       "gather": bool(gather_buf is not None)},
+                       "gather": bool(gather_buf is not None), "auto_reset_episode_length": args.auto_reset or None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": "pp3::env_step_kernel", "bytes_per_env_step": bpe,

@@ -249,7 +249,10 @@ enum {
   PP3_F_METRICS = 4,  /* [N][19] f32: total_dist, scaled rewards */
   PP3_F_DR = 5,       /* [N][62] f32 */
   PP3_F_PIPELINE = 6, /* [N][PP3_PIPE_STRIDE] f32 (when enabled) */
-  PP3_F_ACTION = 7    /* [N][12] f32 scratch action buffer owned by the handle */
+  PP3_F_ACTION = 7,   /* [N][12] f32 scratch action buffer owned by the handle */
+  PP3_F_EPISODE = 8,  /* [N][PP3_EP_STRIDE] f32 episode bookkeeping (auto-reset mode) */
+  PP3_F_FIRST_STATE = 9, /* [N][PP3_FIRST_STRIDE] f32 qpos|qvel|qacc_warmstart of the reset */
+  PP3_F_FIRST_OBS = 10   /* [N][36H] f32 observation of the reset */
 };
 
 /* Optional pipeline-state output (brax State.x / xd of the last substep,
@@ -317,6 +320,25 @@ int pp3_set_pipeline_output(pp3_env_t* env, int32_t enable);
  * state records, with ctrl_dev = f32[N][12] held fixed (no env logic).  Used by
  * the substep parity tests; writes the pipeline record of the last substep. */
 int pp3_physics_step(pp3_env_t* env, const float* ctrl_dev, int32_t nsteps, void* stream);
+
+/* Auto-reset mode = brax.envs.training.wrap(env, episode_length, action_repeat=1) on device
+ * ([ext] brax 0.12.1 EpisodeWrapper + AutoResetWrapper, the wrappers Brax PPO puts around
+ * PupperV3Env).  Per env: episode step counter, truncation flag and the
+ * episode sum_reward / length; pp3_reset stores the reset's qpos/qvel/qacc_warmstart and obs
+ * as the env's "first" state; every pp3_step then
+ *   - zeroes the episode counter if the previous step was done (AutoResetWrapper.step),
+ *   - runs the env step, increments the counter, sets done |= counter >= episode_length and
+ *     truncation = (counter >= episode_length) & !env_done (EpisodeWrapper.step),
+ *   - replaces qpos/qvel/qacc_warmstart and obs by the first state where done (the env's
+ *     info -- rng, command, last action, ... -- carries over, as in Brax).
+ * episode_length <= 0 turns the mode off (plain PupperV3Env.step semantics). */
+#define PP3_EP_STEPS 0
+#define PP3_EP_TRUNCATION 1
+#define PP3_EP_SUM_REWARD 2
+#define PP3_EP_LENGTH 3
+#define PP3_EP_STRIDE 4
+#define PP3_FIRST_STRIDE 55
+int pp3_set_auto_reset(pp3_env_t* env, int32_t episode_length);
 
 /* Device pointer + element count per env of a field (PP3_F_*). */
 int pp3_field(pp3_env_t* env, int32_t field, void** dev_ptr, int64_t* elems_per_env);

@@ -68,6 +68,7 @@ struct alignas(16) Shared {
   float mass[NB], inertia[NB][3], ipos[NB][3];
   float fric, kp, kd;
   int dr_on;
+  float ep[PP3_EP_STRIDE], ep_prev_done;  // auto-reset mode: episode record, previous done
   // kinematics / dynamics of the current substep (the last one feeds the epilogue)
   float xpos[NB][3], xquat[NB][4], xaxis[NJ][3];
   float com[4];
@@ -1441,6 +1442,10 @@ struct StepArgs {
   float* metrics;        // [N][19]
   const float* dr;       // [N][62] or null
   float* pipe;           // [N][PIPE] or null
+  float* episode;        // [N][PP3_EP_STRIDE] (auto-reset mode) or null
+  const float* first_state;  // [N][PP3_FIRST_STRIDE]
+  const float* first_obs;    // [N][36H]
+  int episode_length;
   int N;
 };
 
@@ -1462,6 +1467,11 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (l == 0) s.prof_t = __builtin_amdgcn_s_memtime();
 #endif
   for (int i = l; i < PP3_S_ACT_BUF; i += HW) s.st[i] = gst[i];
+  // auto-reset mode: the previous step's done and this env's episode record (kept in LDS)
+  if (a.episode) {
+    if (l == 0) s.ep_prev_done = a.done[env];
+    if (l < PP3_EP_STRIDE) s.ep[l] = a.episode[(size_t)env * PP3_EP_STRIDE + l];
+  }
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
   SYNC();
   if (l < NQ) s.qpos[l] = s.st[PP3_S_QPOS + l];
@@ -1627,9 +1637,23 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   // ---- state management (environment.py:448-482) ----
   int stepc = (int)s.st[PP3_S_STEP] + 1;
   const bool resample = stepc > m.resample_step;
+  const float reward = fminf(fmaxf(rsum * m.dt, 0.0f), 10000.0f);
+  bool done_out = isdone;
+  if (a.episode) {  // brax EpisodeWrapper.step / AutoResetWrapper.step ([ext] brax 0.12.1)
+    const float keep = 1.0f - s.ep_prev_done;            // previous step done -> counters restart
+    const float ep_rec = l < PP3_EP_STRIDE ? s.ep[l] : 0.0f;
+    const float steps = s.ep[PP3_EP_STEPS] * keep + 1.0f;
+    const bool trunc_hit = steps >= (float)a.episode_length;
+    done_out = isdone || trunc_hit;
+    float v = steps;
+    if (l == PP3_EP_TRUNCATION) v = (trunc_hit && !isdone) ? 1.0f : 0.0f;
+    if (l == PP3_EP_SUM_REWARD) v = (ep_rec + reward) * keep;
+    if (l == PP3_EP_LENGTH) v = (ep_rec + 1.0f) * keep;
+    if (own && l < PP3_EP_STRIDE) a.episode[(size_t)env * PP3_EP_STRIDE + l] = v;
+  }
   if (own && l == 0) {
-    a.reward[env] = fminf(fmaxf(rsum * m.dt, 0.0f), 10000.0f);
-    a.done[env] = isdone ? 1.0f : 0.0f;
+    a.reward[env] = reward;
+    a.done[env] = done_out ? 1.0f : 0.0f;
     a.metrics[(size_t)env * PP3_NMETRIC] =
         sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
   }
@@ -1649,6 +1673,14 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (isdone || resample) stepc = 0;
   if (l == 0) s.st[PP3_S_STEP] = (float)stepc;
   if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
+  if (a.episode && done_out) {  // AutoResetWrapper: pipeline state and obs <- the reset's
+    const float* fs = a.first_state + (size_t)env * PP3_FIRST_STRIDE;
+    for (int i = l; i < PP3_FIRST_STRIDE; i += HW) s.st[PP3_S_QPOS + i] = fs[i];
+    const float* fo = a.first_obs + (size_t)env * PP3_OBS_DIM * m.H;
+    float* oo = a.obs_out + (size_t)env * PP3_OBS_DIM * m.H;
+    if (own)
+      for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) oo[i] = fo[i];
+  }
   SYNC();
   if (own)
     for (int i = l; i < PP3_S_ACT_BUF; i += HW) gst[i] = s.st[i];
@@ -1669,6 +1701,9 @@ struct ResetArgs {
   const uint8_t* mask;   // [N] or null
   const float* dr;
   float* pipe;
+  float* episode;      // auto-reset mode: zeroed
+  float* first_state;  // auto-reset mode: [N][PP3_FIRST_STRIDE] <- this reset
+  float* first_obs;    // auto-reset mode: [N][36H] <- this reset's obs
   int N;
 };
 
@@ -1726,6 +1761,12 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   __syncthreads();  // the gravity row above is global memory written by other lanes
   get_obs(s, m, gst + m.imu_off, l, h, own);
   write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, l, own);
+  if (own && a.episode) {
+    if (l < PP3_EP_STRIDE) a.episode[(size_t)env * PP3_EP_STRIDE + l] = 0.0f;
+    float* fs = a.first_state + (size_t)env * PP3_FIRST_STRIDE;
+    for (int i = l; i < PP3_FIRST_STRIDE; i += HW) fs[i] = s.st[PP3_S_QPOS + i];
+    write_obs(s, m, nullptr, a.first_obs + (size_t)env * PP3_OBS_DIM * m.H, l, true);
+  }
   if (own && l == 0) { a.reward[env] = 0.0f; a.done[env] = 0.0f; }
   if (own && l < PP3_NMETRIC) a.metrics[(size_t)env * PP3_NMETRIC + l] = 0.0f;
   if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
@@ -1806,6 +1847,10 @@ struct pp3_env {
   int pipe_on;
   int nc;  // contact cap (kernel template): 8 on flat terrain, 16 with obstacle geoms
   float* action;
+  float* episode;      // auto-reset mode buffers (null when off)
+  float* first_state;
+  float* first_obs;
+  int episode_length;
   hipEvent_t ev0, ev1;
 };
 
@@ -2168,7 +2213,8 @@ int pp3_destroy(pp3_env_t* e) {
   if (!e) return PP3_OK;
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
-  void* bufs[] = {e->dmodel, e->state, e->obs[0], e->obs[1], e->reward, e->done, e->metrics, e->dr, e->pipe, e->action};
+  void* bufs[] = {e->dmodel, e->state, e->obs[0], e->obs[1], e->reward, e->done, e->metrics, e->dr, e->pipe, e->action,
+                  e->episode, e->first_state, e->first_obs};
   for (void* b : bufs) (void)hipFree(b);
   (void)hipEventDestroy(e->ev0);
   (void)hipEventDestroy(e->ev1);
@@ -2196,6 +2242,9 @@ int pp3_reset(pp3_env_t* e, const uint32_t* keys_dev, const uint8_t* mask_dev, v
   a.mask = mask_dev;
   a.dr = e->dr_on ? e->dr : nullptr;
   a.pipe = e->pipe_on ? e->pipe : nullptr;
+  a.episode = e->episode_length > 0 ? e->episode : nullptr;
+  a.first_state = e->first_state;
+  a.first_obs = e->first_obs;
   a.N = e->N;
   if (e->nc == 8) hipLaunchKernelGGL(env_reset_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   else hipLaunchKernelGGL(env_reset_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
@@ -2217,11 +2266,33 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   a.metrics = e->metrics;
   a.dr = e->dr_on ? e->dr : nullptr;
   a.pipe = e->pipe_on ? e->pipe : nullptr;
+  a.episode = e->episode_length > 0 ? e->episode : nullptr;
+  a.first_state = e->first_state;
+  a.first_obs = e->first_obs;
+  a.episode_length = e->episode_length;
   a.N = e->N;
   if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   else hipLaunchKernelGGL(env_step_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
   e->obs_cur ^= 1;
+  return PP3_OK;
+}
+
+int pp3_set_auto_reset(pp3_env_t* e, int32_t episode_length) {
+  if (!e) return set_err(PP3_ERR_ARG, "null env");
+  HIPCHK(hipSetDevice(e->device));
+  if (episode_length > 0 && !e->episode) {
+    HIPCHK(hipMalloc(&e->episode, sizeof(float) * (size_t)e->N * PP3_EP_STRIDE));
+    HIPCHK(hipMalloc(&e->first_state, sizeof(float) * (size_t)e->N * PP3_FIRST_STRIDE));
+    HIPCHK(hipMalloc(&e->first_obs, sizeof(float) * (size_t)e->N * PP3_OBS_DIM * e->H));
+    HIPCHK(hipMemsetAsync(e->episode, 0, sizeof(float) * (size_t)e->N * PP3_EP_STRIDE, e->stream));
+    // until the next pp3_reset the current state is the "first" state
+    HIPCHK(hipMemcpy2DAsync(e->first_state, sizeof(float) * PP3_FIRST_STRIDE, e->state, sizeof(float) * e->stride,
+                            sizeof(float) * PP3_FIRST_STRIDE, e->N, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->first_obs, e->obs[e->obs_cur], sizeof(float) * (size_t)e->N * PP3_OBS_DIM * e->H,
+                          hipMemcpyDeviceToDevice, e->stream));
+  }
+  e->episode_length = episode_length > 0 ? episode_length : 0;
   return PP3_OK;
 }
 
@@ -2270,6 +2341,9 @@ int pp3_field(pp3_env_t* e, int32_t field, void** ptr, int64_t* elems) {
     case PP3_F_DR: p = e->dr; n = PP3_NDR; break;
     case PP3_F_PIPELINE: p = e->pipe; n = PP3_PIPE_STRIDE; break;
     case PP3_F_ACTION: p = e->action; n = PP3_NU; break;
+    case PP3_F_EPISODE: p = e->episode; n = PP3_EP_STRIDE; break;
+    case PP3_F_FIRST_STATE: p = e->first_state; n = PP3_FIRST_STRIDE; break;
+    case PP3_F_FIRST_OBS: p = e->first_obs; n = (int64_t)PP3_OBS_DIM * e->H; break;
     default: return set_err(PP3_ERR_ARG, "unknown field");
   }
   *ptr = p;

@@ -19,6 +19,9 @@ S_AIR_TIME, S_LAST_CONTACT, S_KICK, S_STEP, S_ACT_BUF = 87, 91, 95, 97, 98
 GEOM_PLANE, GEOM_SPHERE, GEOM_BOX = 0, 2, 6
 
 F_STATE, F_OBS, F_REWARD, F_DONE, F_METRICS, F_DR, F_PIPELINE, F_ACTION = range(8)
+F_EPISODE, F_FIRST_STATE, F_FIRST_OBS = 8, 9, 10
+EP_STEPS, EP_TRUNCATION, EP_SUM_REWARD, EP_LENGTH, EP_STRIDE = 0, 1, 2, 3, 4
+FIRST_STRIDE = 55
 
 P_XPOS, P_XQUAT, P_XD_VEL, P_XD_ANG = 0, 39, 91, 130
 P_SITE_XPOS, P_QFRC_ACT, P_QACC, P_NCON = 169, 181, 199, 217

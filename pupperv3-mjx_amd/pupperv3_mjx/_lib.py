@@ -57,10 +57,12 @@ def load() -> C.CDLL:
     L.pp3_fill_uniform.argtypes = [vp, vp, i64, C.c_uint32, C.c_uint32, C.c_float, C.c_float, vp]
     L.pp3_step_timed.argtypes = [vp, vp, i64, i32, C.POINTER(C.c_float)]
     L.pp3_phase_profile.argtypes = [C.POINTER(C.c_uint64), i32, i32]
+    L.pp3_set_auto_reset.argtypes = [vp, i32]
     for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
                  "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
-                 "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile"):
+                 "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
+                 "pp3_set_auto_reset"):
         getattr(L, name).restype = C.c_int
     if L.pp3_abi_version() != _abi.ABI_VERSION:
         raise PupperHipError("ABI version mismatch between libpupper_hip.so and pupperv3_mjx/_abi.py")
@@ -81,7 +83,7 @@ EXPORTED_SYMBOLS = (
     "pp3_num_envs", "pp3_state_stride", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
     "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
-    "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
+    "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_set_auto_reset",
 )
 
 

@@ -1,0 +1,100 @@
+"""Brax training wrappers for the HIP env, on device.
+
+Brax PPO does not step PupperV3Env directly: `brax.training.agents.ppo.train` wraps it with
+`brax.envs.training.wrap(env, episode_length, action_repeat, randomization_fn)` =
+(DomainRandomization)VmapWrapper -> EpisodeWrapper -> AutoResetWrapper ([ext] brax 0.12.1,
+pinned in requirements.txt:3; not vendored in the reference).  `wrap` below gives the same
+reset()/step() surface with the episode bookkeeping and the auto-reset done inside the fused
+step kernel (pp3_set_auto_reset), so a rollout never leaves the GPU:
+
+  * EpisodeWrapper: info['steps'] counts env steps; done |= steps >= episode_length;
+    info['truncation'] = 1 where the episode length, not the env, ended the episode;
+    info['episode_metrics'] = {'sum_reward', 'length'} (reset to 0 after a done step).
+  * AutoResetWrapper: at the start of a step, steps := 0 where the previous step was done;
+    after it, pipeline_state (qpos, qvel, qacc_warmstart) and obs := the env's first state
+    (the state its last reset produced) where done.  The env's own info (rng, command, last
+    action, latency buffers, ...) carries over, as in Brax.
+
+Domain randomisation (the DomainRandomizationVmapWrapper role) is PupperV3Env.
+set_domain_randomization.  action_repeat > 1 is not supported (the reference trains with 1).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi, _lib
+from .environment import PupperV3Env, State
+
+
+class AutoResetEpisodeEnv:
+    """EpisodeWrapper + AutoResetWrapper semantics over a batched PupperV3Env."""
+
+    def __init__(self, env: PupperV3Env, episode_length: int = 1000, action_repeat: int = 1):
+        if action_repeat != 1:
+            raise NotImplementedError("action_repeat != 1 is not supported on device")
+        if episode_length <= 0:
+            raise ValueError("episode_length must be positive")
+        self.env = env
+        self.episode_length = int(episode_length)
+        _lib.check(env._L.pp3_set_auto_reset(env._h, self.episode_length))
+
+    # brax Env surface
+    @property
+    def observation_size(self) -> int:
+        return self.env.observation_size
+
+    @property
+    def action_size(self) -> int:
+        return self.env.action_size
+
+    @property
+    def dt(self) -> float:
+        return self.env.dt
+
+    @property
+    def unwrapped(self) -> PupperV3Env:
+        return self.env
+
+    def _decorate(self, st: State) -> State:
+        ep = self.env._get(_abi.F_EPISODE)
+        first = self.env._get(_abi.F_FIRST_STATE)
+        fobs = self.env._get(_abi.F_FIRST_OBS)
+        single = np.ndim(st.reward) == 0
+        sq = (lambda v: v[0]) if single else (lambda v: v)
+        st.info["steps"] = sq(ep[:, _abi.EP_STEPS].copy())
+        st.info["truncation"] = sq(ep[:, _abi.EP_TRUNCATION].copy())
+        st.info["episode_metrics"] = {"sum_reward": sq(ep[:, _abi.EP_SUM_REWARD].copy()),
+                                      "length": sq(ep[:, _abi.EP_LENGTH].copy())}
+        st.info["episode_done"] = sq(np.asarray(st.reward) * 0 + np.asarray(st.done))
+        st.info["first_pipeline_state"] = {"q": sq(first[:, 0:19].copy()), "qd": sq(first[:, 19:37].copy()),
+                                           "qacc_warmstart": sq(first[:, 37:55].copy())}
+        st.info["first_obs"] = sq(fobs.copy())
+        return st
+
+    def reset(self, rng) -> State:
+        return self._decorate(self.env.reset(rng))
+
+    def step(self, state: State, action) -> State:
+        n = self.env.num_envs
+        info = state.info
+        if "steps" in info:  # host-side edits of the episode record are honoured
+            ep = np.zeros((n, _abi.EP_STRIDE), dtype=np.float32)
+            ep[:, _abi.EP_STEPS] = np.asarray(info["steps"], dtype=np.float32).reshape(n)
+            ep[:, _abi.EP_TRUNCATION] = np.asarray(info["truncation"], dtype=np.float32).reshape(n)
+            ep[:, _abi.EP_SUM_REWARD] = np.asarray(info["episode_metrics"]["sum_reward"], dtype=np.float32).reshape(n)
+            ep[:, _abi.EP_LENGTH] = np.asarray(info["episode_metrics"]["length"], dtype=np.float32).reshape(n)
+            self.env._put(_abi.F_EPISODE, ep)
+        self.env._put(_abi.F_DONE, np.asarray(state.done, dtype=np.float32).reshape(n, 1))
+        return self._decorate(self.env.step(state, action))
+
+
+def wrap(env: PupperV3Env, episode_length: int = 1000, action_repeat: int = 1,
+         randomization_fn=None, rng=None) -> AutoResetEpisodeEnv:
+    """brax.envs.training.wrap for the HIP env.  `randomization_fn(sys, rng) -> (sys_batched,
+    in_axes)` (domain_randomization.domain_randomize) is applied once with `rng` [N, 2]."""
+    if randomization_fn is not None:
+        if rng is None:
+            raise ValueError("randomization_fn needs rng (one key per env)")
+        sys_b, _ = randomization_fn(env.sys, rng)
+        env.set_domain_randomization(sys_b)
+    return AutoResetEpisodeEnv(env, episode_length, action_repeat)
