@@ -109,6 +109,9 @@ def main():
     ap.add_argument("--gather", action="store_true", help="RCCL all_gather of obs|reward|done per step (configs[3])")
     ap.add_argument("--auto-reset", type=int, default=0, metavar="EPISODE_LENGTH",
                     help="on-device EpisodeWrapper+AutoResetWrapper (brax training wrap) with this episode length")
+    ap.add_argument("--policy", type=str, default="", metavar="H1,H2,...",
+                    help="policy-in-the-loop rollout: an exported-format MLP (random weights, elu) computes the "
+                         "actions from the observation buffer on device before every env step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
@@ -171,11 +174,34 @@ def main():
         if world > 1:
             dist.barrier()
 
+    policy = None
+    if args.policy:
+        from types import SimpleNamespace
+        from collections import OrderedDict
+        from pupperv3_mjx import export
+        rs = np.random.RandomState(7)
+        sizes = [env.observation_size] + [int(v) for v in args.policy.split(",")] + [2 * _abi.NU]
+        layers = OrderedDict((f"hidden_{i}", {"kernel": rs.normal(scale=1 / np.sqrt(sizes[i]), size=(sizes[i], sizes[i + 1])),
+                                              "bias": np.zeros(sizes[i + 1])}) for i in range(len(sizes) - 1))
+        norm = SimpleNamespace(mean=np.zeros(sizes[0]), std=np.ones(sizes[0]))
+        pol = export.convert_params((norm, {"params": layers}), "elu", 0.75, 5.0, 0.25, np.zeros(12), np.ones(12),
+                                    -np.ones(12), True, env._observation_history, 30.0, 30.0)
+        policy = export.DevicePolicy(pol, local_rank)
+        for _ in range(args.warmup):
+            policy.act_env(env, acts.ptr.value)
+            env.step_device(acts.ptr.value)
+
     barrier()
     torch.cuda.synchronize()
     env.synchronize()
     t0 = time.perf_counter()
-    if gather_buf is None:
+    if policy is not None:
+        for i in range(args.steps):
+            policy.act_env(env, acts.ptr.value)
+            env.step_device(acts.ptr.value)
+        env.synchronize()
+        kernel_ms = (time.perf_counter() - t0) * 1e3  # policy + env step per iteration (no per-kernel events)
+    elif gather_buf is None:
         _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + args.warmup * E * 12 * 4), E * 12,
                                     args.steps, C.byref(ms)))
         kernel_ms = ms.value
@@ -237,7 +263,8 @@ def main():
                                        "domain randomisation" if args.dr else "no DR")),
                        "envs_per_gpu": E, "global_envs": E * world, "obs_history": env._observation_history,
                        "n_frames": env._n_frames, "parallelism": f"env-sharded x{world} (no data-path collective)",
-                       "gather": bool(gather_buf is not None), "auto_reset_episode_length": args.auto_reset or None},
+                       "gather": bool(gather_buf is not None), "auto_reset_episode_length": args.auto_reset or None,
+                       "policy_in_loop": args.policy or None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": "pp3::env_step_kernel", "bytes_per_env_step": bpe,

@@ -346,6 +346,8 @@ int pp3_field(pp3_env_t* env, int32_t field, void** dev_ptr, int64_t* elems_per_
 int pp3_copy_field_to_host(pp3_env_t* env, int32_t field, void* host, size_t bytes);
 int pp3_copy_field_from_host(pp3_env_t* env, int32_t field, const void* host, size_t bytes);
 int pp3_synchronize(pp3_env_t* env);
+/* The handle's own HIP stream (hipStream_t), for ordering other work (e.g. pp3_policy_act) with it. */
+void* pp3_stream(pp3_env_t* env);
 
 /* Small device-memory helpers so a host can run without any other GPU runtime. */
 int pp3_device_malloc(int32_t device, size_t bytes, void** out);
@@ -367,6 +369,27 @@ int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stri
 /* Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-clock totals of env_step_kernel
  * summed over envs (n <= 16 slots); returns PP3_ERR_ARG in the production build. */
 int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset);
+
+/* ---------------------------------------------------------------------------------------
+ * On-device MLP policy in the reference's deployment format (export.py:13-81 convert_params:
+ * "layers": dense, "weights": [kernel [in][out], bias [out]], normalisation folded into the
+ * first layer, final layer = Gaussian-head mean, "activation" per layer, final tanh).
+ * pupperv3_mjx/export.py loads such a dict into this API.  Batch forward on the f32 matrix
+ * cores (csrc/pp3_policy.hip).
+ * ------------------------------------------------------------------------------------- */
+typedef struct pp3_policy pp3_policy_t;
+#define PP3_POLICY_MAX_LAYERS 8
+#define PP3_POLICY_MAX_WIDTH 576 /* >= 36 * 15 (observation_history 15) */
+enum { PP3_ACT_LINEAR = 0, PP3_ACT_RELU = 1, PP3_ACT_ELU = 2, PP3_ACT_TANH = 3, PP3_ACT_SIGMOID = 4 };
+/* weights = for each layer: kernel [in][out] row-major, then bias [out] (host memory). */
+int pp3_policy_create(int32_t device, int32_t in_dim, int32_t n_layers, const int32_t* out_dims,
+                      const int32_t* activations, const float* weights, pp3_policy_t** out);
+/* actions[i][0:out_dim] = policy(obs[i][0:in_dim]) for i < n (device pointers, strides in floats). */
+int pp3_policy_act(pp3_policy_t* policy, const float* obs_dev, int64_t obs_stride, int32_t n,
+                   float* actions_dev, int64_t action_stride, void* stream);
+int pp3_policy_out_dim(const pp3_policy_t* policy);
+int pp3_policy_destroy(pp3_policy_t* policy);
+const char* pp3_policy_last_error(void);
 
 #ifdef __cplusplus
 }

@@ -2278,6 +2278,8 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   return PP3_OK;
 }
 
+void* pp3_stream(pp3_env_t* e) { return e ? (void*)e->stream : nullptr; }
+
 int pp3_set_auto_reset(pp3_env_t* e, int32_t episode_length) {
   if (!e) return set_err(PP3_ERR_ARG, "null env");
   HIPCHK(hipSetDevice(e->device));

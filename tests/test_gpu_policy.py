@@ -1,0 +1,63 @@
+"""On-device policy (csrc/pp3_policy.hip, f32 MFMA) vs the numpy meaning of the exported JSON
+(export.policy_forward, float64).  Tolerance: |d| <= 2e-5 * (1 + |y|) (fp32 products and
+accumulation, K <= 540)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import common
+from pupperv3_mjx import _abi, _lib, export
+from pupperv3_mjx.environment import PupperV3Env, make_keys
+from test_export import _brax_like_params
+
+pytestmark = pytest.mark.gpu
+
+
+def _policy(sizes, act, seed=0):
+    rs = np.random.RandomState(seed)
+    return export.convert_params(_brax_like_params(rs, sizes), act, 0.75, 5.0, 0.25, np.zeros(12), np.ones(12),
+                                 -np.ones(12), True, (sizes[0] // 36), 30.0, 30.0)
+
+
+@pytest.mark.parametrize("sizes,act,n", [([72, 256, 128, 128, 24], "elu", 37), ([540, 512, 256, 24], "relu", 64),
+                                         ([72, 64, 24], "sigmoid", 16), ([72, 128, 128, 24], "tanh", 1)])
+def test_device_policy_matches_numpy(require_gpu, sizes, act, n):
+    pol = _policy(sizes, act)
+    dp = export.DevicePolicy(pol)
+    x = np.random.RandomState(1).normal(size=(n, sizes[0])).astype(np.float32)
+    xb = _lib.DeviceBuffer(x.nbytes)
+    yb = _lib.DeviceBuffer(n * 12 * 4)
+    try:
+        xb.upload(x)
+        dp.act(xb.ptr.value, sizes[0], n, yb.ptr.value, 12)
+        y = np.zeros((n, 12), dtype=np.float32)
+        _lib.check(_lib.load().pp3_memcpy_d2h(y.ctypes.data_as(C.c_void_p), yb.ptr, y.nbytes))
+        want = export.policy_forward(pol, x.astype(np.float64))
+        assert np.all(np.abs(y - want) <= 2e-5 * (1 + np.abs(want))), np.abs(y - want).max()
+    finally:
+        xb.free(); yb.free(); dp.close()
+
+
+def test_policy_env_rollout_on_device(require_gpu, tmp_path):
+    """policy(obs buffer) -> actions -> env step, 20 times without host round trips."""
+    path = common.write_model(tmp_path, 0)
+    n = 32
+    e = PupperV3Env(**common.fixture_kwargs(path), num_envs=n)
+    pol = _policy([72, 128, 128, 24], "elu")
+    dp = export.DevicePolicy(pol)
+    ab = _lib.DeviceBuffer(n * 12 * 4)
+    try:
+        st = e.reset(make_keys(0, n))
+        dp.act_env(e, ab.ptr.value)
+        a = np.zeros((n, 12), dtype=np.float32)
+        e.synchronize()
+        _lib.check(_lib.load().pp3_memcpy_d2h(a.ctypes.data_as(C.c_void_p), ab.ptr, a.nbytes))
+        assert np.all(np.abs(a - export.policy_forward(pol, st.obs)) <= 2e-5 * (1 + np.abs(a)))
+        for _ in range(20):
+            dp.act_env(e, ab.ptr.value)
+            e.step_device(ab.ptr.value)
+        e.synchronize()
+        assert np.all(np.isfinite(e._get(_abi.F_OBS))) and np.all(np.isfinite(e._get(_abi.F_REWARD)))
+    finally:
+        ab.free(); dp.close(); e.close()
