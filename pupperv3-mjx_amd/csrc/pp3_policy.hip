@@ -71,18 +71,37 @@ __global__ __launch_bounds__(64 * NWAVE) void mlp_kernel(Net net, const float* _
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
       const int ar = lane & 15, kk = lane >> 4;
       const float* wc = L.w + c0 + (lane & 15);
+      // chunks of CH k blocks: all CH weight loads (L2 latency) are in flight together, then
+      // CH MFMAs run back to back on two alternating accumulators
+      constexpr int CH = 16;
       int k0 = 0;
-      // unrolled so several k blocks' weight loads (L2 latency) are in flight per MFMA pair
-#pragma unroll 4
-      for (; k0 + 8 <= L.Kp; k0 += 8) {
-        const float a0 = X[ar][k0 + kk], a1 = X[ar][k0 + 4 + kk];
-        const float b0 = wc[(size_t)(k0 + kk) * L.Mp], b1 = wc[(size_t)(k0 + 4 + kk) * L.Mp];
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc1, 0, 0, 0);
+      for (; k0 + 4 * CH <= L.Kp; k0 += 4 * CH) {
+        float av[CH], bv[CH];
+#pragma unroll
+        for (int q = 0; q < CH; q++) {
+          bv[q] = wc[(size_t)(k0 + 4 * q + kk) * L.Mp];
+          av[q] = X[ar][k0 + 4 * q + kk];
+        }
+#pragma unroll
+        for (int q = 0; q < CH; q += 2) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], acc, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q + 1], bv[q + 1], acc1, 0, 0, 0);
+        }
       }
-      if (k0 < L.Kp) {
-        const float a0 = X[ar][k0 + kk], b0 = wc[(size_t)(k0 + kk) * L.Mp];
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc, 0, 0, 0);
+      {  // tail (< CH blocks): predicated loads, same shape
+        float av[CH], bv[CH];
+#pragma unroll
+        for (int q = 0; q < CH; q++) {
+          const bool in = k0 + 4 * q < L.Kp;
+          bv[q] = in ? wc[(size_t)(k0 + 4 * q + kk) * L.Mp] : 0.0f;
+          av[q] = in ? X[ar][k0 + 4 * q + kk] : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < CH; q += 2) {
+          if (k0 + 4 * q >= L.Kp) break;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], acc, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q + 1], bv[q + 1], acc1, 0, 0, 0);
+        }
       }
       acc += acc1;
       const int col = c0 + (lane & 15);
