@@ -188,7 +188,7 @@ typedef struct pp3_env_config_t {
   int32_t n_torso_geoms;
   int32_t torso_geoms[8];
   int32_t rng_partitionable;   /* jax_threefry_partitionable (jax 0.5.0: 1) */
-  int32_t ncon_max;            /* contact cap per env: 0 = auto (8 flat, 16 with boxes), 8, 16 */
+  int32_t ncon_max;            /* contact cap per env (deepest kept): 0 = default 8, 8, 16 */
   double latency_dist[PP3_MAX_LAG];
   double imu_latency_dist[PP3_MAX_LAG];
   double action_scale;

@@ -98,7 +98,7 @@ static int g_partitionable = 1;
 static _Thread_local double g_dbg[512];
 static _Thread_local int g_boundary = 0;  /* near-switch constraint rows seen since the last orc_boundary_take() */
 #define BOUNDARY_REL ((real)1e-4)  /* last Newton iteration's intermediates (debugging aid) */
-static int g_ncon_max = 0; /* contact cap shared with the HIP kernel: 0 = auto (8 flat, 16 with boxes) */
+static int g_ncon_max = 0; /* contact cap shared with the HIP kernel: 0 = default 8 */
 
 /* jax.random.split(key, n)[i] */
 static key_t2 split_i(key_t2 key, int n, int i) {
@@ -403,12 +403,7 @@ static void model_from_abi(Model* M, const pp3_model_t* m, const real* dr) {
       M->act_ctrlrange[a][k] = (real)m->actuator_ctrlrange[a][k];
     }
   }
-  {
-    int has_static_solid = 0;
-    for (int g = 0; g < m->ncgeom; g++)
-      if (m->cgeom_bodyid[g] == 0 && m->cgeom_type[g] != PP3_GEOM_PLANE) has_static_solid = 1;
-    M->ncon_max = g_ncon_max > 0 ? g_ncon_max : (has_static_solid ? 16 : 8);
-  }
+  M->ncon_max = g_ncon_max > 0 ? g_ncon_max : 8; /* same default cap as the kernel (8 deepest) */
   if (dr) {
     /* domain_randomization.py:21-66: one friction scalar for all geoms, Kp/Kd for all
      * actuators, torso COM shift, elementwise inertia / mass scales (values absolute). */

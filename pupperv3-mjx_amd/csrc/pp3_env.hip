@@ -2176,10 +2176,9 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   e->stride = hm.stride;
   e->H = hm.H;
   {
-    int has_static_solid = 0;
-    for (int g = 0; g < model->ncgeom; g++)
-      if (model->cgeom_bodyid[g] == 0 && model->cgeom_type[g] != PP3_GEOM_PLANE) has_static_solid = 1;
-    e->nc = cfg->ncon_max > 0 ? cfg->ncon_max : (has_static_solid ? 16 : 8);
+    // contact cap: 8 deepest per env by default, flat or with obstacle boxes (the reference's
+    // MJX keeps max_contact_points = 5, test_pupper_model.xml:227-230); 16 on request
+    e->nc = cfg->ncon_max > 0 ? cfg->ncon_max : 8;
     if (e->nc != 8 && e->nc != 16) {
       delete e;
       return set_err(PP3_ERR_ARG, "ncon_max must be 0 (auto), 8 or 16");

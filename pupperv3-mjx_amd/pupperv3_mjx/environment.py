@@ -195,7 +195,7 @@ class PupperV3Env:
         c.n_torso_geoms = len(tg)
         c.torso_geoms[:len(tg)] = tg
         c.rng_partitionable = int(rng_partitionable)
-        c.ncon_max = int(max_contacts)  # 0 = auto (8 flat, 16 with static boxes); else 8 or 16
+        c.ncon_max = int(max_contacts)  # contact cap, deepest kept: 0 = default 8; else 8 or 16
         c.latency_dist[:c.latency_len] = [float(v) for v in self._latency_distribution]
         c.imu_latency_dist[:c.imu_latency_len] = [float(v) for v in self._imu_latency_distribution]
         c.action_scale = float(action_scale)

@@ -49,14 +49,15 @@ def _physics_compare(env, m, qpos, qvel, qws, ctrl, nsteps, ncon_max=0):
     return gp, op
 
 
-@pytest.mark.parametrize("nsteps", [1, 3])
-def test_sphere_box_contact_parity(box_path, nsteps):
-    e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=64)
+@pytest.mark.parametrize("nsteps,cap", [(1, 0), (3, 0), (1, 16), (3, 16)])
+def test_sphere_box_contact_parity(box_path, nsteps, cap):
+    """cap 0 = default contact cap (8 deepest); 16 = the larger kernel instance."""
+    e = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=64, max_contacts=cap)
     try:
         m = e.sys_model.struct
-        assert e.config_struct.ncon_max == 0
+        assert e.config_struct.ncon_max == cap
         qpos, qvel, qws, ctrl = common.states_on_boxes(m, 64, seed=nsteps)
-        gp, op = _physics_compare(e, m, qpos, qvel, qws, ctrl, nsteps)
+        gp, op = _physics_compare(e, m, qpos, qvel, qws, ctrl, nsteps, ncon_max=cap)
         if nsteps == 1:
             boxes = _box_ids(m)
             n_box = 0
