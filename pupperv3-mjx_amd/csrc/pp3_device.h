@@ -18,6 +18,21 @@ constexpr int NLMAX = 24;                 // joint-limit rows (12 joints x 2 sid
 constexpr int NFR = 12;                   // frictionloss rows (hinge dofs)
 constexpr int MAX_ROBOT_GEOM = 16;        // DevModel table size for collidable geoms on moving bodies
 constexpr int NMPAIR_MAX = 128;           // nonzero (i, j<=i) entries of M
+constexpr int NMPAIR = 117;               // ... for the 13-body quadruped tree (21 base + 4 x 24 leg)
+constexpr int PAIR_REC = 24;              // floats per flattened collision-pair record
+
+// Flattened narrow-phase record of one candidate pair (host precomputed, one 96-byte row per
+// pair so a lane fetches everything with six 16-byte loads): kind, robot-geom slots (-1 =
+// static), radii, margin, static positions, static frame (plane / box), box half sizes.
+enum { PK_PLANE_SPHERE = 0, PK_SPHERE_SPHERE = 1, PK_SPHERE_BOX = 2 };
+struct alignas(16) PairRec {
+  int32_t kind, s1, s2;
+  float r1, r2, margin;
+  float p1[3], p2[3];
+  float R[9];
+  float half[3];
+};
+static_assert(sizeof(PairRec) == PAIR_REC * 4, "PairRec layout");
 constexpr float MINVAL = 1e-15f;
 constexpr float MINIMP = 0.0001f;
 constexpr float MAXIMP = 0.9999f;
@@ -75,6 +90,8 @@ struct DevModel {
   float pair_margin[PP3_MAX_PAIR];
   float pair_tran[PP3_MAX_PAIR];       // body_invweight0 translational sum
   int32_t pair_sup[PP3_MAX_PAIR];      // Jacobian column support: leg 0..3 (+base), 4 base only, 5 dense
+  uint32_t pair_dm[PP3_MAX_PAIR][2];   // dof masks (ancestor-or-self) of the pair's two bodies
+  PairRec pair_rec[PP3_MAX_PAIR];
   float pair_solimp[PP3_MAX_PAIR][5];  // clamped
   // ---- sites ----
   int32_t nsite;

@@ -83,6 +83,7 @@ struct alignas(16) Shared {
   // contacts
   int ncon, nhit, nl;
   int con_pair[NC], con_sup[NC];
+  uint32_t con_dm[NC][2];  // dof masks of the contact's two bodies
   float con_dist[NC], con_mu[NC];
   float con_G[NC][5];
   float Jc[NC][3][NV];
@@ -328,50 +329,46 @@ __device__ __forceinline__ void make_frame(float f[9], const float nin[3]) {
   for (int k = 0; k < 3; k++) { f[k] = a[k]; f[3 + k] = y[k]; f[6 + k] = z[k]; }
 }
 
-// narrow phase for pair p; returns hit and fills dist/pos/normal
+// narrow phase for pair p; returns hit and fills dist/pos/normal.  One dependent global level:
+// the pair's flattened record (PairRec), then robot-geom world positions from LDS.
 template <int NC>
 __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, int p, float& dist, float pos[3],
                                        float nrm[3]) {
-  const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-  const int t1 = m.cg_type[g1], t2 = m.cg_type[g2];
-  const float margin = m.pair_margin[p];
+  const PairRec rec = m.pair_rec[p];
+  const float margin = rec.margin;
   float p1[3], p2[3];
-  const int s1 = m.cg_slot[g1], s2 = m.cg_slot[g2];
-  {  // robot geoms: world position from LDS; static geoms: from the model (separate loads so
-     // the select is on values, not on an LDS/global pointer, which would become a flat load)
-    const int i1 = s1 >= 0 ? s1 : 0, i2 = s2 >= 0 ? s2 : 0;
-    float l1[3], l2[3], c1[3], c2[3];
+  {  // robot geoms: world position from LDS; static geoms: from the record (value select)
+    const int i1 = rec.s1 >= 0 ? rec.s1 : 0, i2 = rec.s2 >= 0 ? rec.s2 : 0;
     for (int k = 0; k < 3; k++) {
-      l1[k] = s.gxpos[i1][k]; l2[k] = s.gxpos[i2][k];
-      c1[k] = m.cg_pos[g1][k]; c2[k] = m.cg_pos[g2][k];
+      const float l1 = s.gxpos[i1][k], l2 = s.gxpos[i2][k];
+      p1[k] = rec.s1 >= 0 ? l1 : rec.p1[k];
+      p2[k] = rec.s2 >= 0 ? l2 : rec.p2[k];
     }
-    for (int k = 0; k < 3; k++) { p1[k] = s1 >= 0 ? l1[k] : c1[k]; p2[k] = s2 >= 0 ? l2[k] : c2[k]; }
   }
-  if (t1 == PP3_GEOM_PLANE && t2 == PP3_GEOM_SPHERE) {
-    const float* R1 = m.cg_wmat[g1];
-    float nz[3] = {R1[2], R1[5], R1[8]};
-    float v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
-    float r = m.cg_size[g2][0];
+  if (rec.kind == PK_PLANE_SPHERE) {
+    const float nz[3] = {rec.R[2], rec.R[5], rec.R[8]};
+    const float v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    const float r = rec.r2;
     dist = dot3(nz, v) - r;
     if (dist > margin) return false;
     for (int k = 0; k < 3; k++) { nrm[k] = nz[k]; pos[k] = p2[k] - nz[k] * (r + 0.5f * dist); }
     return true;
   }
-  if (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_SPHERE) {
-    float v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
-    float r1 = m.cg_size[g1][0], r2 = m.cg_size[g2][0];
-    float len = sqrtf(dot3(v, v));
+  if (rec.kind == PK_SPHERE_SPHERE) {
+    const float v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    const float r1 = rec.r1, r2 = rec.r2;
+    const float len = sqrtf(dot3(v, v));
     dist = len - r1 - r2;
     if (dist > margin) return false;
     if (len < MINVAL) { nrm[0] = 1; nrm[1] = 0; nrm[2] = 0; }
-    else { float il = 1.0f / len; nrm[0] = v[0] * il; nrm[1] = v[1] * il; nrm[2] = v[2] * il; }
+    else { const float il = 1.0f / len; nrm[0] = v[0] * il; nrm[1] = v[1] * il; nrm[2] = v[2] * il; }
     for (int k = 0; k < 3; k++) pos[k] = p1[k] + nrm[k] * (r1 + 0.5f * dist);
     return true;
   }
-  if (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_BOX) {
-    const float* R2 = m.cg_wmat[g2];
-    const float* hh = m.cg_size[g2];
-    float r = m.cg_size[g1][0];
+  if (rec.kind == PK_SPHERE_BOX) {
+    const float* R2 = rec.R;
+    const float* hh = rec.half;
+    const float r = rec.r1;
     float rel[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]}, dl[3], cl[3];
     for (int k = 0; k < 3; k++) dl[k] = R2[k] * rel[0] + R2[3 + k] * rel[1] + R2[6 + k] * rel[2];
     bool inside = true;
@@ -411,6 +408,8 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const DevModel& m, 
                                               const float pos[3], const float nrm[3]) {
   s.con_pair[slot] = p;
   s.con_sup[slot] = m.pair_sup[p];
+  s.con_dm[slot][0] = m.pair_dm[p][0];
+  s.con_dm[slot][1] = m.pair_dm[p][1];
   s.con_dist[slot] = dist;
   for (int k = 0; k < 3; k++) s.x.a.con_pos[slot][k] = pos[k];
   make_frame(s.x.a.con_frame[slot], nrm);
@@ -841,7 +840,8 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(2);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
-  for (int p = l; p < m.nmpair; p += HW) {
+#pragma unroll
+  for (int p = l; p < NMPAIR; p += HW) {  // compile-time trip count: all index loads issued up front
     const int i = m.mp_i[p], j = m.mp_j[p];
     float v = 0;
 #pragma unroll
@@ -854,14 +854,12 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   const int ncon = s.ncon;
   for (int it = l; it < ncon * NV; it += HW) {
     const int c = it / NV, i = it - c * NV;
-    const int p = s.con_pair[c];
-    const int b1 = m.cg_body[m.pair_g1[p]], b2 = m.cg_body[m.pair_g2[p]];
     const uint32_t bit = 1u << i;
     const float off[3] = {s.x.a.con_pos[c][0] - s.com[0], s.x.a.con_pos[c][1] - s.com[1], s.x.a.con_pos[c][2] - s.com[2]};
     const float* cd = s.cdof[i];
     float cr[3], jp[3];
     cross3(cr, cd, off);
-    const float w = ((m.body_dofmask[b2] & bit) ? 1.0f : 0.0f) - ((m.body_dofmask[b1] & bit) ? 1.0f : 0.0f);
+    const float w = ((s.con_dm[c][1] & bit) ? 1.0f : 0.0f) - ((s.con_dm[c][0] & bit) ? 1.0f : 0.0f);
     for (int k = 0; k < 3; k++) jp[k] = w * (cd[3 + k] + cr[k]);
     const float* fr = s.x.a.con_frame[c];
     s.Jc[c][0][i] = fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2];
@@ -1990,6 +1988,7 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
       np++;
     }
   d->nmpair = np;
+  if (np != NMPAIR) return set_err(PP3_ERR_MODEL, "mass-matrix sparsity differs from the 13-body quadruped tree");
   // collision geoms
   d->ncgeom = mm->ncgeom;
   int nslot = 0;
@@ -2055,6 +2054,26 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
       else if (c2 == 4) sup = c1;
       else sup = 5;
       d->pair_sup[p] = sup < 0 ? 5 : sup;
+    }
+    d->pair_dm[p][0] = d->body_dofmask[mm->cgeom_bodyid[g1]];
+    d->pair_dm[p][1] = d->body_dofmask[mm->cgeom_bodyid[g2]];
+    {  // flattened narrow-phase record
+      PairRec& r = d->pair_rec[p];
+      memset(&r, 0, sizeof(r));
+      const int t1 = mm->cgeom_type[g1], t2 = mm->cgeom_type[g2];
+      r.kind = (t1 == PP3_GEOM_PLANE && t2 == PP3_GEOM_SPHERE) ? PK_PLANE_SPHERE
+               : (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_SPHERE) ? PK_SPHERE_SPHERE
+               : (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_BOX) ? PK_SPHERE_BOX : -1;
+      r.s1 = d->cg_slot[g1];
+      r.s2 = d->cg_slot[g2];
+      r.r1 = d->cg_size[g1][0];
+      r.r2 = d->cg_size[g2][0];
+      r.margin = d->pair_margin[p];
+      for (int k = 0; k < 3; k++) { r.p1[k] = d->cg_pos[g1][k]; r.p2[k] = d->cg_pos[g2][k]; }
+      const int gf = r.kind == PK_SPHERE_BOX ? g2 : g1;  // plane frame / box frame
+      for (int k = 0; k < 9; k++) r.R[k] = d->cg_wmat[gf][k];
+      if (r.kind == PK_SPHERE_BOX)
+        for (int k = 0; k < 3; k++) r.half[k] = d->cg_size[g2][k];
     }
     if (mm->cgeom_margin[g1] != 0 || mm->cgeom_margin[g2] != 0) return set_err(PP3_ERR_MODEL, "nonzero geom margins unsupported");
   }
