@@ -1345,6 +1345,7 @@ __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float*
     s.x.e.u[l] = l < 30 ? v * scale : v;
   }
   SYNC();
+  PHASE(17);
   if (l < 6) {  // one IMU channel per lane
     float inv[4] = {1, 0, 0, 0}, angl[3] = {0, 0, 0};
     if (m.use_imu) {
@@ -1378,6 +1379,7 @@ __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float*
     s.x.e.o[24 + j] = fminf(fmaxf(b, -100.0f), 100.0f);
   }
   SYNC();
+  PHASE(18);
 }
 
 template <int NC>

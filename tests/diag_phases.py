@@ -19,8 +19,8 @@ from pupperv3_mjx.environment import PupperV3Env, make_keys  # noqa: E402
 
 NAMES = ["kinematics", "com/cinert/cdof", "limit/friction rows+actuation", "M+bias+contactJ", "LDL(M)+solve",
          "warmstart", "newton update+grad", "LDL(H)+solve", "line search", "integrate",
-         "prologue", "obs", "rewards+state", "bias+contact edge rows", "hessian build", "crb*cdof+rne chain",
-         "collision"]
+         "prologue", "write_obs (history)", "rewards+state", "bias+contact edge rows", "hessian build",
+         "crb*cdof+rne chain", "collision", "obs rng draws", "imu + lag buffers"]
 
 
 def main():
