@@ -139,3 +139,34 @@ def test_domain_randomized_step_parity(model_path):
         fb.finish()
     finally:
         e.close()
+
+
+def test_legacy_rng_split_parity(model_path):
+    """jax_threefry_partitionable=False (jax 0.5.0's legacy split/bits layout): reset + steps
+    bit-exact in the RNG words and commands against the oracle."""
+    n = 8
+    e = PupperV3Env(**common.fixture_kwargs(model_path), num_envs=n, rng_partitionable=False)
+    try:
+        keys = make_keys(6, n, partitionable=False)
+        st = e.reset(keys)
+        oe = O.OracleEnv(e.sys_model.struct, e.config_struct, precision="f32")
+        orr = [oe.reset(keys[i]) for i in range(n)]
+        orec = np.array([G.oracle_state_to_record(r["state"]) for r in orr])
+        np.testing.assert_array_equal(_rng_words(st._record), _rng_words(orec))
+        np.testing.assert_array_equal(st.info["command"], orec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3])
+        rs = np.random.RandomState(2)
+        fb = G.FlipBudget(max_frac=0.1)
+        for t in range(5):
+            a = rs.uniform(-1, 1, size=(n, 12)).astype(np.float32)
+            prev = st
+            st = e.step(prev, a)
+            for i in range(n):
+                o = oe.step(dict(state=G.record_to_oracle_state(prev._record[i]), obs=prev.obs[i].astype(np.float64)),
+                            a[i].astype(np.float64))
+                orr_i = G.oracle_state_to_record(o["state"])
+                np.testing.assert_array_equal(_rng_words(st._record[i:i + 1]), _rng_words(orr_i[None]))
+                np.testing.assert_array_equal(st._record[i, _abi.S_KICK:_abi.S_KICK + 2], orr_i[_abi.S_KICK:_abi.S_KICK + 2])
+                fb.check(np.abs(st.obs[i] - o["obs"]).max() <= 5e-3, o, f"step {t} env {i}")
+        fb.finish()
+    finally:
+        e.close()
