@@ -841,7 +841,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   PHASE(2);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
 #pragma unroll
-  for (int p = l; p < NMPAIR; p += HW) {  // compile-time trip count: all index loads issued up front
+  for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count: index loads issued up front
+    const int p = l + HW * t;
+    if (p >= NMPAIR) continue;
     const int i = m.mp_i[p], j = m.mp_j[p];
     float v = 0;
 #pragma unroll
@@ -1466,7 +1468,14 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (l < NPROF) s.prof[l] = 0;
   if (l == 0) s.prof_t = __builtin_amdgcn_s_memtime();
 #endif
-  for (int i = l; i < PP3_S_ACT_BUF; i += HW) s.st[i] = gst[i];
+  {  // state record head: all loads in flight together (compile-time trip count)
+    float v[(PP3_S_ACT_BUF + HW - 1) / HW];
+#pragma unroll
+    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++) v[t] = l + HW * t < PP3_S_ACT_BUF ? gst[l + HW * t] : 0.0f;
+#pragma unroll
+    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
+      if (l + HW * t < PP3_S_ACT_BUF) s.st[l + HW * t] = v[t];
+  }
   // auto-reset mode: the previous step's done and this env's episode record (kept in LDS)
   if (a.episode) {
     if (l == 0) s.ep_prev_done = a.done[env];
@@ -1683,7 +1692,9 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   }
   SYNC();
   if (own)
-    for (int i = l; i < PP3_S_ACT_BUF; i += HW) gst[i] = s.st[i];
+#pragma unroll
+    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
+      if (l + HW * t < PP3_S_ACT_BUF) gst[l + HW * t] = s.st[l + HW * t];
   PHASE(12);
 #ifdef PP3_PHASE_PROF
   if (l < NPROF) atomicAdd(&g_prof[l], (unsigned long long)s.prof[l]);
@@ -1772,7 +1783,9 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
   SYNC();
   if (own)
-    for (int i = l; i < PP3_S_ACT_BUF; i += HW) gst[i] = s.st[i];
+#pragma unroll
+    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
+      if (l + HW * t < PP3_S_ACT_BUF) gst[l + HW * t] = s.st[l + HW * t];
 }
 
 struct PhysArgs {
