@@ -1284,6 +1284,18 @@ __device__ __forceinline__ float push_lagged(float* row, int n, float v, int li,
   return out;
 }
 
+// push_lagged with the row's old values already loaded (prefetched at kernel start)
+__device__ __forceinline__ float push_lagged_pre(float* row, int n, float v, int li, bool store, const float* old) {
+  float out = v;
+#pragma unroll
+  for (int q = 0; q < PP3_MAX_LAG; q++) {
+    const float nv = q == 0 ? v : old[q - 1];
+    if (store && q < n) row[q] = nv;
+    out = (q == li) ? nv : out;
+  }
+  return out;
+}
+
 // sample_command (environment.py:246-272): lanes 0..6 draw, lane 0 writes out[3]
 __device__ __forceinline__ void sample_command(const DevModel& m, Key rng, float* out, int l, int h) {
   const int part = m.partitionable;
@@ -1330,7 +1342,8 @@ __device__ __forceinline__ void sample_orientation(const DevModel& m, Key rng, f
 // _get_obs (environment.py:485-543): consumes the st rng, pushes the IMU buffer (HBM row
 // gimu = [6][Li]), writes s.x.e.o[36]
 template <int NC>
-__device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int l, int h, bool store) {
+__device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int l, int h, bool store,
+                                        const float* imu_stash = nullptr) {
   const int part = m.partitionable;
   const Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
   const Key kl = split_i(rng, 6, l < 6 ? l : 0, part);  // lane i holds split(rng, 6)[i]
@@ -1361,7 +1374,15 @@ __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float*
     const float gn = sqrtf(dot3(g, g));
     const float v = l < 3 ? angl[l] + s.x.e.u[l] : g[l - 3] / gn;
     const int li = choice_from_uniform(m.imu_lat_dist, m.Li, s.x.e.u[30]);
-    const float lagged = push_lagged(gimu + l * m.Li, m.Li, v, li, store);
+    float lagged;
+    if (imu_stash) {  // the row's old values were fetched at kernel start (one memory round trip)
+      float old[PP3_MAX_LAG];
+#pragma unroll
+      for (int q = 0; q < PP3_MAX_LAG; q++) old[q] = imu_stash[PP3_MAX_LAG * l + q];
+      lagged = push_lagged_pre(gimu + l * m.Li, m.Li, v, li, store, old);
+    } else {
+      lagged = push_lagged(gimu + l * m.Li, m.Li, v, li, store);
+    }
     s.x.e.o[l] = fminf(fmaxf(lagged, -100.0f), 100.0f);
   }
   if (l == 6) {
@@ -1468,7 +1489,33 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (l < NPROF) s.prof[l] = 0;
   if (l == 0) s.prof_t = __builtin_amdgcn_s_memtime();
 #endif
-  {  // state record head: all loads in flight together (compile-time trip count)
+  // ---- every global load of this env step issued together (one memory round trip): state
+  // record head, this lane's action-latency row and IMU row, the action, the obs history ----
+  const float* act_env = a.actions + (size_t)env * NU;
+  float arow[PP3_MAX_LAG], irow[PP3_MAX_LAG], act_in = 0.0f;
+  {
+    const float* ar = gst + PP3_S_ACT_BUF + (l < NU ? l : 0) * m.La;
+    const float* ir = gst + m.imu_off + (l < 6 ? l : 0) * m.Li;
+#pragma unroll
+    for (int q = 0; q < PP3_MAX_LAG; q++) {
+      arow[q] = (l < NU && q < m.La) ? ar[q] : 0.0f;
+      irow[q] = (l < 6 && q < m.Li) ? ir[q] : 0.0f;
+    }
+    if (l < NU) act_in = act_env[l];
+  }
+  {  // observation history: obs_out[36:] = obs_in[:36(H-1)] (environment.py:540-543)
+    const int nmove = PP3_OBS_DIM * (m.H - 1);
+    const float* oi = a.obs_in + (size_t)env * PP3_OBS_DIM * m.H;
+    float* oo = a.obs_out + (size_t)env * PP3_OBS_DIM * m.H;
+    float tmp[OBS_MOVE];
+#pragma unroll
+    for (int t = 0; t < OBS_MOVE; t++) tmp[t] = (l + HW * t < nmove) ? oi[l + HW * t] : 0.0f;
+    if (own)
+#pragma unroll
+      for (int t = 0; t < OBS_MOVE; t++)
+        if (l + HW * t < nmove) oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
+  }
+  {  // state record head
     float v[(PP3_S_ACT_BUF + HW - 1) / HW];
 #pragma unroll
     for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++) v[t] = l + HW * t < PP3_S_ACT_BUF ? gst[l + HW * t] : 0.0f;
@@ -1506,12 +1553,18 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     s.st[PP3_S_RNG] = __uint_as_float(k_new.a);
     s.st[PP3_S_RNG + 1] = __uint_as_float(k_new.b);
   }
-  const float* act_env = a.actions + (size_t)env * NU;
   if (l < NU) {
-    const float lagged = push_lagged(gst + PP3_S_ACT_BUF + l * m.La, m.La, act_env[l], li, own);
+    const float lagged = push_lagged_pre(gst + PP3_S_ACT_BUF + l * m.La, m.La, act_in, li, own, arow);
     const float t = m.default_pose[l] + lagged * m.action_scale;
     s.ctrl[l] = fminf(fmaxf(t, m.jlo[l]), m.jhi[l]);
   }
+  SYNC();
+  // the state head's qpos|qvel|qacc_ws words are copied out (above) and only rewritten after the
+  // observation, so they hold the IMU rows' old values meanwhile (6 x MAX_LAG <= 55 floats)
+  float* imu_stash = s.st + PP3_S_QPOS;
+  if (l < 6)
+#pragma unroll
+    for (int q = 0; q < PP3_MAX_LAG; q++) imu_stash[PP3_MAX_LAG * l + q] = irow[q];
   SYNC();
   PHASE(10);
   // ---- physics: n_frames x mj_step (environment.py:366) ----
@@ -1523,12 +1576,18 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     asm volatile("" : "+s"(mp));
     substep(s, *(const DevModel*)mp, l, h, true);
   }
+  SYNC();
+  // ---- observation (history already shifted in the prologue) ----
+  get_obs(s, m, gst + m.imu_off, l, h, own, imu_stash);
+  {
+    float* oo = a.obs_out + (size_t)env * PP3_OBS_DIM * m.H;
+    if (own)
+      for (int k = l; k < PP3_OBS_DIM; k += HW) oo[k] = s.x.e.o[k];
+  }
+  SYNC();
   if (l < NQ) s.st[PP3_S_QPOS + l] = s.qpos[l];
   if (l < NV) { s.st[PP3_S_QVEL + l] = s.qvel[l]; s.st[PP3_S_QACC_WS + l] = s.qws[l]; }
   SYNC();
-  // ---- observation ----
-  get_obs(s, m, gst + m.imu_off, l, h, own);
-  write_obs(s, m, a.obs_in + (size_t)env * PP3_OBS_DIM * m.H, a.obs_out + (size_t)env * PP3_OBS_DIM * m.H, l, own);
   PHASE(11);
   // ---- brax x/xd (lanes 1..13), feet (16..19) ----
   if (l >= 1 && l < NB) {
@@ -1687,6 +1746,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     for (int i = l; i < PP3_FIRST_STRIDE; i += HW) s.st[PP3_S_QPOS + i] = fs[i];
     const float* fo = a.first_obs + (size_t)env * PP3_OBS_DIM * m.H;
     float* oo = a.obs_out + (size_t)env * PP3_OBS_DIM * m.H;
+    __threadfence_block();  // the prologue's history stores (other lanes, same addresses) land first
     if (own)
       for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) oo[i] = fo[i];
   }
