@@ -119,13 +119,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the multi-rank path on a single GPU (never used by the driver):
+    # PP3_BENCH_DEVICE pins every rank to one device, PP3_BENCH_BACKEND=gloo avoids RCCL's
+    # one-rank-per-GPU rule
+    device = int(os.environ.get("PP3_BENCH_DEVICE", local_rank))
+    backend = os.environ.get("PP3_BENCH_BACKEND", "nccl")
     # torch first: its bundled libamdhip64.so.7 then also serves libpupper_hip.so (one HIP runtime)
     import torch
     import torch.distributed as dist
     import numpy as np
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     from pupperv3_mjx import MODEL_XML, _abi, _lib, sharding
     from pupperv3_mjx.environment import PupperV3Env
@@ -142,7 +150,7 @@ def main():
         tree.write(model_path, encoding="unicode")
 
     E = args.envs
-    env = PupperV3Env(**bench_kwargs(model_path), num_envs=E, device=local_rank, pipeline_output=False)
+    env = PupperV3Env(**bench_kwargs(model_path), num_envs=E, device=device, pipeline_output=False)
     L = env._L
     if args.dr:
         from pupperv3_mjx import domain_randomization as dr, rng
@@ -158,7 +166,7 @@ def main():
     init_obs = st.obs.copy()
 
     total = args.warmup + args.steps
-    acts = _lib.DeviceBuffer(total * E * 12 * 4, local_rank)
+    acts = _lib.DeviceBuffer(total * E * 12 * 4, device)
     _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, total * E * 12, 1234 + rank, 0, -1.0, 1.0, None))
     env.synchronize()
     ms = C.c_float()
@@ -186,7 +194,7 @@ def main():
         norm = SimpleNamespace(mean=np.zeros(sizes[0]), std=np.ones(sizes[0]))
         pol = export.convert_params((norm, {"params": layers}), "elu", 0.75, 5.0, 0.25, np.zeros(12), np.ones(12),
                                     -np.ones(12), True, env._observation_history, 30.0, 30.0)
-        policy = export.DevicePolicy(pol, local_rank)
+        policy = export.DevicePolicy(pol, device)
         for _ in range(args.warmup):
             policy.act_env(env, acts.ptr.value)
             env.step_device(acts.ptr.value)
@@ -221,7 +229,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
+    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, kernel_ms_max = float(t[0]), float(t[1])
