@@ -195,3 +195,34 @@ def test_max_history_and_latency_lengths(box_path):
         fb.finish()
     finally:
         e.close()
+
+
+def test_results_independent_of_batch_layout(box_path):
+    """Envs are independent: the same keys and actions give bit-identical records, obs, rewards
+    and dones whether the envs run in one handle or split over two handles (the sharded
+    multi-GPU layout; shards start at even env ids, so wave partners are unchanged).  An odd
+    split changes wave partners; then an env whose partner has a leg-leg contact takes the dense
+    factorisation with it and may differ at the rounding level."""
+    n, split = 64, 32
+    kw = common.fixture_kwargs(box_path, terminal_body_z=0.0, kick_probability=0.5)
+    full = PupperV3Env(**kw, num_envs=n)
+    a_part = PupperV3Env(**kw, num_envs=split)
+    b_part = PupperV3Env(**kw, num_envs=n - split)
+    try:
+        keys = make_keys(11, n)
+        s_full = full.reset(keys)
+        s_a = a_part.reset(keys[:split])
+        s_b = b_part.reset(keys[split:])
+        rs = np.random.RandomState(7)
+        for _ in range(12):
+            act = rs.uniform(-2, 2, size=(n, 12)).astype(np.float32)
+            s_full = full.step(s_full, act)
+            s_a = a_part.step(s_a, act[:split])
+            s_b = b_part.step(s_b, act[split:])
+            rec = np.concatenate([s_a._record, s_b._record])
+            np.testing.assert_array_equal(s_full._record.view(np.uint32), rec.view(np.uint32))
+            np.testing.assert_array_equal(s_full.obs, np.concatenate([s_a.obs, s_b.obs]))
+            np.testing.assert_array_equal(s_full.reward, np.concatenate([s_a.reward, s_b.reward]))
+            np.testing.assert_array_equal(s_full.done, np.concatenate([s_a.done, s_b.done]))
+    finally:
+        full.close(); a_part.close(); b_part.close()
