@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--dr", action="store_true", help="domain randomisation on (configs[2])")
     ap.add_argument("--obstacles", type=int, default=0, help="obstacles.py boxes (configs[4])")
+    ap.add_argument("--terrain", action="store_true",
+                    help="per-env terrain (SURVEY 8f rank 3): every env gets its own random boxes in the --obstacles slots")
     ap.add_argument("--gather", action="store_true", help="RCCL all_gather of obs|reward|done per step (configs[3])")
     ap.add_argument("--auto-reset", type=int, default=0, metavar="EPISODE_LENGTH",
                     help="on-device EpisodeWrapper+AutoResetWrapper (brax training wrap) with this episode length")
@@ -156,6 +158,12 @@ def main():
         from pupperv3_mjx import domain_randomization as dr, rng
         sysb, _ = dr.domain_randomize(env.sys, rng.split(rng.PRNGKey(1000 + rank), E))
         env.set_domain_randomization(sysb)
+    if args.terrain:
+        from pupperv3_mjx import obstacles
+        if not args.obstacles:
+            raise SystemExit("--terrain needs --obstacles N (the box-geom slots)")
+        env.set_terrain(obstacles.sample_terrain(E, args.obstacles, (-5, 5), (-5, 5), height=0.02, length=6.0,
+                                                 seed=args.seed * 1000 + rank, min_boxes=args.obstacles // 2))
     if args.auto_reset > 0:
         _lib.check(L.pp3_set_auto_reset(env._h, args.auto_reset))
     keys = sharding.shard_keys(args.seed, E * world, world, rank)  # global env ids, contiguous shards
@@ -271,6 +279,7 @@ def main():
                                        "domain randomisation" if args.dr else "no DR")),
                        "envs_per_gpu": E, "global_envs": E * world, "obs_history": env._observation_history,
                        "n_frames": env._n_frames, "parallelism": f"env-sharded x{world} (no data-path collective)",
+                       "per_env_terrain": bool(args.terrain),
                        "gather": bool(gather_buf is not None), "auto_reset_episode_length": args.auto_reset or None,
                        "policy_in_loop": args.policy or None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -316,6 +316,17 @@ int pp3_step(pp3_env_t* env, const float* actions_dev, void* stream);
 int pp3_set_dr(pp3_env_t* env, const float* dr_dev);
 int pp3_set_pipeline_output(pp3_env_t* env, int32_t enable);
 
+/* Per-env terrain (the reference's obstacles.py:16-57 boxes are static and
+ * shared by all envs).  The model's world-body box geoms become per-env slots: boxes_host =
+ * f32[N][n_boxes][PP3_TERRAIN_BOX] host array, per box pos[3] (world), quat[4] (w,x,y,z, any
+ * norm) and half sizes[3]; a box whose half sizes are all <= 0 is absent in that env, so envs
+ * may hold different numbers of boxes.  n_boxes must equal the model's world box-geom count
+ * (pp3_terrain_slots).  Contact parameters (friction, solref, solimp) stay the model's.
+ * boxes_host = NULL returns to the model's static boxes.  Synchronises the handle's stream. */
+#define PP3_TERRAIN_BOX 10
+int pp3_set_terrain(pp3_env_t* env, const float* boxes_host, int32_t n_boxes);
+int32_t pp3_terrain_slots(const pp3_env_t* env);
+
 /* Raw physics: `nsteps` x mj_step on the qpos/qvel/qacc_warmstart stored in the
  * state records, with ctrl_dev = f32[N][12] held fixed (no env logic).  Used by
  * the substep parity tests; writes the pipeline record of the last substep. */

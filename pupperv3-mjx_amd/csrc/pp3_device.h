@@ -33,6 +33,15 @@ struct alignas(16) PairRec {
   float half[3];
 };
 static_assert(sizeof(PairRec) == PAIR_REC * 4, "PairRec layout");
+// One per-env terrain box (host packed from pos/quat/half): world centre, world rotation
+// (row-major), half sizes; 64 bytes = four 16-byte loads.
+struct alignas(16) TerrainRec {
+  float p[3];
+  float R[9];
+  float half[3];
+  float pad;
+};
+static_assert(sizeof(TerrainRec) == 64, "TerrainRec layout");
 constexpr float MINVAL = 1e-15f;
 constexpr float MINIMP = 0.0001f;
 constexpr float MAXIMP = 0.9999f;
@@ -91,8 +100,11 @@ struct DevModel {
   float pair_tran[PP3_MAX_PAIR];       // body_invweight0 translational sum
   int32_t pair_sup[PP3_MAX_PAIR];      // Jacobian column support: leg 0..3 (+base), 4 base only, 5 dense
   uint32_t pair_dm[PP3_MAX_PAIR][2];   // dof masks (ancestor-or-self) of the pair's two bodies
-  PairRec pair_rec[PP3_MAX_PAIR];
+  PairRec pair_rec[PP3_MAX_PAIR];      // sphere-box: s2 = -1 - (box slot)
   float pair_solimp[PP3_MAX_PAIR][5];  // clamped
+  // per-env terrain (pp3_set_terrain): TerrainRec[N (padded even)][nbox], or 0 = static boxes
+  uint64_t terrain;
+  int32_t nbox;
   // ---- sites ----
   int32_t nsite;
   int32_t site_body[PP3_MAX_SITE];

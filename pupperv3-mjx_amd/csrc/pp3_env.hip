@@ -17,11 +17,13 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "pp3_device.h"
 
@@ -366,8 +368,20 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, i
     return true;
   }
   if (rec.kind == PK_SPHERE_BOX) {
-    const float* R2 = rec.R;
-    const float* hh = rec.half;
+    float R2[9], hh[3];
+    for (int k = 0; k < 9; k++) R2[k] = rec.R[k];
+    for (int k = 0; k < 3; k++) hh[k] = rec.half[k];
+    if (m.terrain) {  // per-env terrain: this env's box in slot -1 - s2 (rows padded to an even env count)
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(1))) const v4f GF4;
+      const int env_raw = 2 * blockIdx.x + (threadIdx.x >> 5);
+      const GF4* t = (const GF4*)(uintptr_t)m.terrain + ((size_t)env_raw * m.nbox + (-1 - rec.s2)) * 4;
+      const v4f t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+      p2[0] = t0.x; p2[1] = t0.y; p2[2] = t0.z;
+      R2[0] = t0.w; R2[1] = t1.x; R2[2] = t1.y; R2[3] = t1.z; R2[4] = t1.w;
+      R2[5] = t2.x; R2[6] = t2.y; R2[7] = t2.z; R2[8] = t2.w;
+      hh[0] = t3.x; hh[1] = t3.y; hh[2] = t3.z;
+    }
     const float r = rec.r1;
     float rel[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]}, dl[3], cl[3];
     for (int k = 0; k < 3; k++) dl[k] = R2[k] * rel[0] + R2[3 + k] * rel[1] + R2[6 + k] * rel[2];
@@ -1924,6 +1938,8 @@ struct pp3_env {
   float* first_state;
   float* first_obs;
   int episode_length;
+  float* terrain;  // TerrainRec rows (pp3_set_terrain), null until first set
+  int nbox;        // world box-geom slots in the model
   hipEvent_t ev0, ev1;
 };
 
@@ -2067,7 +2083,11 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
   // collision geoms
   d->ncgeom = mm->ncgeom;
   int nslot = 0;
+  int box_slot[PP3_MAX_CGEOM];
+  d->nbox = 0;
+  d->terrain = 0;
   for (int g = 0; g < mm->ncgeom; g++) {
+    box_slot[g] = (mm->cgeom_bodyid[g] == 0 && mm->cgeom_type[g] == PP3_GEOM_BOX) ? d->nbox++ : -1;
     d->cg_type[g] = mm->cgeom_type[g];
     d->cg_body[g] = mm->cgeom_bodyid[g];
     d->cg_id[g] = mm->cgeom_id[g];
@@ -2140,7 +2160,7 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
                : (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_SPHERE) ? PK_SPHERE_SPHERE
                : (t1 == PP3_GEOM_SPHERE && t2 == PP3_GEOM_BOX) ? PK_SPHERE_BOX : -1;
       r.s1 = d->cg_slot[g1];
-      r.s2 = d->cg_slot[g2];
+      r.s2 = r.kind == PK_SPHERE_BOX ? -1 - box_slot[g2] : d->cg_slot[g2];
       r.r1 = d->cg_size[g1][0];
       r.r2 = d->cg_size[g2][0];
       r.margin = d->pair_margin[p];
@@ -2269,6 +2289,7 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   e->N = num_envs;
   e->stride = hm.stride;
   e->H = hm.H;
+  e->nbox = hm.nbox;
   {
     // contact cap: 8 deepest per env by default, flat or with obstacle boxes (the reference's
     // MJX keeps max_contact_points = 5, test_pupper_model.xml:227-230); 16 on request
@@ -2307,7 +2328,7 @@ int pp3_destroy(pp3_env_t* e) {
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->dmodel, e->state, e->obs[0], e->obs[1], e->reward, e->done, e->metrics, e->dr, e->pipe, e->action,
-                  e->episode, e->first_state, e->first_obs};
+                  e->episode, e->first_state, e->first_obs, e->terrain};
   for (void* b : bufs) (void)hipFree(b);
   (void)hipEventDestroy(e->ev0);
   (void)hipEventDestroy(e->ev1);
@@ -2397,6 +2418,53 @@ int pp3_set_dr(pp3_env_t* e, const float* dr_dev) {
   if (!dr_dev) { e->dr_on = 0; return PP3_OK; }
   HIPCHK(hipMemcpyAsync(e->dr, dr_dev, (size_t)e->N * PP3_NDR * sizeof(float), hipMemcpyDeviceToDevice, e->stream));
   e->dr_on = 1;
+  return PP3_OK;
+}
+
+int32_t pp3_terrain_slots(const pp3_env_t* e) { return e ? e->nbox : 0; }
+
+int pp3_set_terrain(pp3_env_t* e, const float* boxes, int32_t n_boxes) {
+  if (!e) return set_err(PP3_ERR_ARG, "null env");
+  HIPCHK(hipSetDevice(e->device));
+  uint64_t ptr = 0;
+  if (boxes) {
+    if (n_boxes != e->nbox)
+      return set_err(PP3_ERR_ARG, "pp3_set_terrain: n_boxes must equal the model's world box-geom count (" +
+                                      std::to_string(e->nbox) + ")");
+    if (n_boxes == 0) return set_err(PP3_ERR_ARG, "pp3_set_terrain: the model has no box geoms to use as slots");
+    const size_t rows = (size_t)(e->N + 1) / 2 * 2;  // even: the kernel indexes by 2 * block + half
+    std::vector<TerrainRec> rec(rows * n_boxes);
+    memset(rec.data(), 0, rec.size() * sizeof(TerrainRec));
+    for (size_t i = 0; i < rows; i++)
+      for (int b = 0; b < n_boxes; b++) {
+        TerrainRec& r = rec[i * n_boxes + b];
+        if (i >= (size_t)e->N) {  // padding row: absent boxes
+          r.p[2] = -1e4f;
+          continue;
+        }
+        const float* x = boxes + (i * n_boxes + b) * PP3_TERRAIN_BOX;
+        if (!(x[7] > 0 || x[8] > 0 || x[9] > 0)) {  // absent: far below the floor, zero size
+          r.p[2] = -1e4f;
+          r.R[0] = r.R[4] = r.R[8] = 1.0f;
+          continue;
+        }
+        double q[4] = {x[3], x[4], x[5], x[6]};
+        const double qn = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        if (!(qn > 0)) return set_err(PP3_ERR_ARG, "pp3_set_terrain: zero quaternion");
+        for (int k = 0; k < 4; k++) q[k] /= qn;
+        double R[9];
+        quat2mat_d(q, R);
+        for (int k = 0; k < 3; k++) { r.p[k] = x[k]; r.half[k] = x[7 + k]; }
+        for (int k = 0; k < 9; k++) r.R[k] = (float)R[k];
+      }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (!e->terrain) HIPCHK(hipMalloc(&e->terrain, rows * n_boxes * sizeof(TerrainRec)));
+    HIPCHK(hipMemcpy(e->terrain, rec.data(), rec.size() * sizeof(TerrainRec), hipMemcpyHostToDevice));
+    ptr = (uint64_t)(uintptr_t)e->terrain;
+  } else {
+    HIPCHK(hipStreamSynchronize(e->stream));
+  }
+  HIPCHK(hipMemcpy((char*)e->dmodel + offsetof(DevModel, terrain), &ptr, sizeof(ptr), hipMemcpyHostToDevice));
   return PP3_OK;
 }
 

@@ -19,6 +19,7 @@ S_AIR_TIME, S_LAST_CONTACT, S_KICK, S_STEP, S_ACT_BUF = 87, 91, 95, 97, 98
 GEOM_PLANE, GEOM_SPHERE, GEOM_BOX = 0, 2, 6
 
 F_STATE, F_OBS, F_REWARD, F_DONE, F_METRICS, F_DR, F_PIPELINE, F_ACTION = range(8)
+TERRAIN_BOX = 10  # PP3_TERRAIN_BOX: pos[3], quat[4] (w,x,y,z), half sizes[3]
 F_EPISODE, F_FIRST_STATE, F_FIRST_OBS = 8, 9, 10
 EP_STEPS, EP_TRUNCATION, EP_SUM_REWARD, EP_LENGTH, EP_STRIDE = 0, 1, 2, 3, 4
 FIRST_STRIDE = 55

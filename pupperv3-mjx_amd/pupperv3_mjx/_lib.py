@@ -65,11 +65,15 @@ def load() -> C.CDLL:
     L.pp3_policy_last_error.restype = C.c_char_p
     L.pp3_stream.argtypes = [vp]
     L.pp3_stream.restype = vp
+    L.pp3_set_terrain.argtypes = [vp, vp, i32]
+    L.pp3_terrain_slots.argtypes = [vp]
+    L.pp3_terrain_slots.restype = i32
     for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
                  "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
                  "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
-                 "pp3_set_auto_reset", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy"):
+                 "pp3_set_auto_reset", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy",
+                 "pp3_set_terrain"):
         getattr(L, name).restype = C.c_int
     if L.pp3_abi_version() != _abi.ABI_VERSION:
         raise PupperHipError("ABI version mismatch between libpupper_hip.so and pupperv3_mjx/_abi.py")
@@ -92,7 +96,7 @@ EXPORTED_SYMBOLS = (
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
     "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_set_auto_reset",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
-    "pp3_stream",
+    "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
 )
 
 

@@ -294,6 +294,23 @@ class PupperV3Env:
             raise ValueError("DR batch size must equal num_envs")
         _lib.check(self._L.pp3_copy_field_from_host(self._h, _abi.F_DR, table.ctypes.data_as(C.c_void_p), table.nbytes))
 
+    # ------------------------------------------------------------------ terrain
+    @property
+    def terrain_slots(self) -> int:
+        """World box geoms in the model (obstacles.add_boxes_to_model); each is a per-env slot."""
+        return int(self._L.pp3_terrain_slots(self._h))
+
+    def set_terrain(self, boxes: Optional[np.ndarray]) -> None:
+        """Per-env terrain boxes f32[num_envs, terrain_slots, 10] (pos, quat wxyz, half sizes;
+        all-zero half sizes = absent), or None for the model's static boxes (pp3_set_terrain)."""
+        if boxes is None:
+            _lib.check(self._L.pp3_set_terrain(self._h, None, 0))
+            return
+        b = np.ascontiguousarray(boxes, dtype=np.float32)
+        if b.ndim != 3 or b.shape[0] != self.num_envs or b.shape[2] != _abi.TERRAIN_BOX:
+            raise ValueError(f"terrain must be [num_envs, n_boxes, {_abi.TERRAIN_BOX}], got {b.shape}")
+        _lib.check(self._L.pp3_set_terrain(self._h, b.ctypes.data_as(C.c_void_p), b.shape[1]))
+
     # ------------------------------------------------------------------ device API
     def device_field(self, field_id: int) -> Tuple[int, int]:
         """(device pointer, elements per env) of a PP3_F_* buffer."""

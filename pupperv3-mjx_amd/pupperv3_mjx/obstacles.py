@@ -64,3 +64,37 @@ def add_boxes_to_model(tree: ET.ElementTree, n_boxes: int, x_range: Tuple, y_ran
         }
         ET.SubElement(world, "geom", attrs)
     return tree
+
+
+# --------------------------------------------------------------------------- per-env terrain
+# the reference's boxes are static and shared; here every env may hold its
+# own boxes in the model's box-geom slots (PupperV3Env.set_terrain / pp3_set_terrain).  A row
+# is pos[3], quat[4] (w,x,y,z), half sizes[3]; all-zero half sizes mark an absent box.
+
+def terrain_from_specs(specs: Sequence[BoxSpec], num_envs: int):
+    """Every env gets the same boxes (the reference's static layout, as per-env rows)."""
+    import numpy as np
+    row = np.array([[b.x, b.y, 0.0, *b.quat, *b.half_sizes] for b in specs], dtype=np.float32)
+    return np.ascontiguousarray(np.broadcast_to(row, (num_envs,) + row.shape))
+
+
+def sample_terrain(num_envs: int, n_boxes: int, x_range: Sequence[float], y_range: Sequence[float],
+                   height: float = 0.02, depth: float = 0.02, length: float = 3.0, seed: int = 0,
+                   min_boxes: int = None):
+    """Independent boxes per env, each drawn like obstacles.py:16-57 draws one box (x, y
+    uniform, yaw uniform in [-pi, pi], half sizes (depth/2, length/2, height)), from a numpy
+    Generator seeded with `seed`.  With `min_boxes`, env i keeps a uniform number of boxes in
+    [min_boxes, n_boxes] and the rest of its slots are absent (variable contact counts)."""
+    import numpy as np
+    g = np.random.default_rng(seed)
+    x = g.uniform(x_range[0], x_range[1], size=(num_envs, n_boxes))
+    y = g.uniform(y_range[0], y_range[1], size=(num_envs, n_boxes))
+    half = g.uniform(-math.pi, math.pi, size=(num_envs, n_boxes)) / 2
+    t = np.zeros((num_envs, n_boxes, 10), dtype=np.float32)
+    t[..., 0], t[..., 1] = x, y
+    t[..., 3], t[..., 6] = np.cos(half), np.sin(half)
+    t[..., 7], t[..., 8], t[..., 9] = depth / 2.0, length / 2.0, height
+    if min_boxes is not None:
+        keep = g.integers(min_boxes, n_boxes + 1, size=num_envs)
+        t[np.arange(n_boxes)[None, :] >= keep[:, None], 7:10] = 0.0
+    return t

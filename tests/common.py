@@ -139,3 +139,55 @@ def states_with_self_contact(model, jnt_range, n, seed=0, z=0.5):
     qpos = np.array(qs)
     qvel = rs.normal(scale=0.3, size=(n, 18))
     return qpos, qvel, np.zeros((n, 18)), qpos[:, 7:].copy()
+
+
+def terrain_slots(model):
+    """cgeom indices of the world box geoms, in slot order (pp3_set_terrain)."""
+    return [g for g in range(model.ncgeom) if model.cgeom_bodyid[g] == 0 and model.cgeom_type[g] == _abi.GEOM_BOX]
+
+
+def model_terrain_rows(model):
+    """The model's own static boxes as one terrain row f32[n_boxes, 10]."""
+    return np.array([[*model.cgeom_pos[g][:], *model.cgeom_quat[g][:], *model.cgeom_size[g][:]]
+                     for g in terrain_slots(model)], dtype=np.float32)
+
+
+def model_with_terrain(model, rows):
+    """Copy of the model struct whose box geoms hold one env's terrain rows (the oracle's view of
+    a per-env terrain; absent boxes are parked below the floor with zero size, as on the device)."""
+    m = type(model).from_buffer_copy(model)
+    for b, g in enumerate(terrain_slots(model)):
+        r = np.asarray(rows[b], dtype=np.float64)
+        if not np.any(r[7:10] > 0):
+            pos, quat, size = (0.0, 0.0, -1e4), (1.0, 0.0, 0.0, 0.0), (0.0, 0.0, 0.0)
+        else:
+            q = r[3:7] / np.linalg.norm(r[3:7])
+            pos, quat, size = r[0:3], q, r[7:10]
+        for k in range(3):
+            m.cgeom_pos[g][k] = pos[k]
+            m.cgeom_size[g][k] = size[k]
+        for k in range(4):
+            m.cgeom_quat[g][k] = quat[k]
+    return m
+
+
+def terrain_under(xy, n_boxes, seed=0, absent_p=0.3):
+    """Per-env terrain f32[n, n_boxes, 10]: slot 0 is a rail (obstacles.py sizes) straddled by
+    the robot at xy[i], slot 1 a second rail crossing nearby, the other slots random boxes of
+    the reference's distribution or (probability absent_p) absent."""
+    rs = np.random.RandomState(seed)
+    n = xy.shape[0]
+    t = obstacles.sample_terrain(n, n_boxes, (-5, 5), (-5, 5), seed=seed)
+    for i in range(n):
+        for slot in (0, 1):
+            yaw = rs.uniform(-np.pi, np.pi)
+            ax = np.array([-np.sin(yaw), np.cos(yaw)])  # rail's long (local y) axis in world
+            nrm = np.array([np.cos(yaw), np.sin(yaw)])
+            c = xy[i] + nrm * rs.uniform(-0.12, 0.12) + ax * rs.uniform(-1.0, 1.0)
+            t[i, slot, 0:3] = (c[0], c[1], 0.0)
+            t[i, slot, 3:7] = (np.cos(yaw / 2), 0.0, 0.0, np.sin(yaw / 2))
+            t[i, slot, 7:10] = (0.01, 1.5, 0.02)
+        for slot in range(2, n_boxes):
+            if rs.uniform() < absent_p:
+                t[i, slot, 7:10] = 0.0
+    return t

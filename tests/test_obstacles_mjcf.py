@@ -92,3 +92,36 @@ def test_unsupported_features_fail_loudly():
     xml = open(MODEL_XML).read().replace('cone="pyramidal"', 'cone="elliptic"')
     with pytest.raises(NotImplementedError):
         mjcf.load(xml, is_string=True)
+
+
+def test_sample_terrain_distribution_and_absent_slots():
+    """Per-env terrain rows follow one obstacles.py:16-57 box draw per slot."""
+    t = obstacles.sample_terrain(256, 10, (-5, 5), (-4, 4), height=0.02, depth=0.02, length=6.0, seed=3, min_boxes=2)
+    assert t.shape == (256, 10, 10) and t.dtype == np.float32
+    present = np.any(t[..., 7:10] > 0, axis=2)
+    assert present[:, :2].all() and not present.all()  # at least min_boxes, some absent
+    p = t[present]
+    assert np.all(np.abs(p[:, 0]) <= 5) and np.all(np.abs(p[:, 1]) <= 4) and np.all(p[:, 2] == 0)
+    np.testing.assert_allclose(np.linalg.norm(p[:, 3:7], axis=1), 1, atol=1e-6)
+    assert np.all(p[:, 4:6] == 0)
+    np.testing.assert_allclose(p[:, 7:10], np.broadcast_to([0.01, 3.0, 0.02], p[:, 7:10].shape), rtol=1e-6)
+    a = obstacles.sample_terrain(4, 10, (-5, 5), (-5, 5), seed=0)
+    b = obstacles.sample_terrain(4, 10, (-5, 5), (-5, 5), seed=0)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_terrain_from_specs_equals_model_boxes(tmp_path):
+    """The static reference layout as terrain rows == the compiled model's box geoms, and the
+    oracle's per-env-terrain model view of those rows reproduces the model's physics."""
+    from oracle import oracle as O
+    path = common.write_model(tmp_path, 10)
+    m = mjcf.load(path).struct
+    specs = obstacles.sample_boxes(10, (-5, 5), (-5, 5), height=0.02, length=6.0, seed=0)
+    rows = obstacles.terrain_from_specs(specs, 3)
+    np.testing.assert_allclose(rows[1], common.model_terrain_rows(m), rtol=0, atol=1e-6)
+    mt = common.model_with_terrain(m, common.model_terrain_rows(m))
+    qpos, qvel, qws, ctrl = common.states_on_boxes(m, 4, seed=1)
+    for i in range(4):
+        a = O.mj_step(m, qpos[i], qvel[i], qws[i], ctrl[i], nsteps=2)
+        b = O.mj_step(mt, qpos[i], qvel[i], qws[i], ctrl[i], nsteps=2)
+        np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-6)
