@@ -567,7 +567,17 @@ __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m,
 // loads, so each trailing update is one v_fma with VGPR operands.  col = 20 floats, 16-byte
 // aligned, owned by this half.
 // ------------------------------------------------------------------------------------
+// The lane index made opaque at the top of a routine: its lane-index masks (l == k, l > k, ...)
+// are then recomputed per call (one v_cmp each) instead of being hoisted out of the substep
+// loop as ~100 live 64-bit SGPR masks that spill to VGPR lanes (two v_readlane per use).
+__device__ __forceinline__ int opaque_lane(int l) {
+  asm volatile("" : "+v"(l));
+  __builtin_assume(l >= 0 && l < HW);
+  return l;
+}
+
 __device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int l, float* col) {
+  l = opaque_lane(l);
   const int slot = l < NV ? l : NV;  // lanes >= NV carry copies of row NV-1: dummy slot
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -591,6 +601,7 @@ __device__ __forceinline__ void ldl_rows(float (&a)[NV], float& dinv, int l, flo
 // solve L D L^T x = b; x = b_i on entry (lane i).  Uses s.x.L for the transposed factor.
 template <int NC>
 __device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int l, int h) {
+  l = opaque_lane(l);
   const int li = l < NV ? l : NV - 1;
 #pragma unroll
   for (int k = 0; k < NV; ++k)
@@ -625,6 +636,7 @@ __host__ __device__ constexpr int pnat(int p) { return p < 12 ? p + 6 : p - 12; 
 __host__ __device__ constexpr int npos(int d) { return d < 6 ? d + 12 : d - 6; }   // dof -> permuted
 
 __device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, float* col /* >= 80 floats */) {
+  l = opaque_lane(l);
   const int slot = l < NV ? l : NV;
 #pragma unroll
   for (int st = 0; st < 3; st++) {
@@ -680,6 +692,7 @@ __device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, fl
 template <int NC>
 __device__ __forceinline__ float ldl_solve_arrow(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int l,
                                                  int h) {
+  l = opaque_lane(l);
   const int lp = l < NV ? l : NV - 1;
   const int leg = lp < 12 ? lp / 3 : 4, li = lp - 3 * (lp < 12 ? leg : 0);  // leg index, level in leg
 #pragma unroll
@@ -790,18 +803,19 @@ __device__ __forceinline__ int choice_from_uniform(const float* dist, int n, flo
 template <int NC>
 __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
+  l = opaque_lane(l);
   kinematics(s, m, l);
   SYNC();
-  PHASE(0);
+  PHASE(0); l = opaque_lane(l);
   com_pos(s, m, l, h);
   SYNC();
-  PHASE(1);
+  PHASE(1); l = opaque_lane(l);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
   crb_times_cdof(s, m, l);
   rne_chain(s, m, l);
-  PHASE(15);
+  PHASE(15); l = opaque_lane(l);
   collision(s, m, l, h);
-  PHASE(16);
+  PHASE(16); l = opaque_lane(l);
   {
     // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
     bool act = false;
@@ -852,7 +866,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     if (l < 6) s.qfrc_act[l] = 0.0f;
   }
   SYNC();
-  PHASE(2);
+  PHASE(2); l = opaque_lane(l);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
 #pragma unroll
   for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count: index loads issued up front
@@ -883,7 +897,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     s.Jc[c][2][i] = fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2];
   }
   SYNC();
-  PHASE(3);
+  PHASE(3); l = opaque_lane(l);
   // ---- phase 5: qfrc_bias/smooth (subtree sums of body forces), contact edge rows ----
   if (l < NV) {
     float cf[6];
@@ -922,7 +936,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     s.efc_aref[r] = -m.pair_b[p] * vel - m.pair_k[p] * imp * (dist - m.pair_margin[p]);
   }
   SYNC();
-  PHASE(13);
+  PHASE(13); l = opaque_lane(l);
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
   {
     const int lp = l < NV ? l : NV - 1, dn = pnat(lp);  // permuted row held by this lane
@@ -934,7 +948,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     if (l < NV) s.qacc_smooth[dn] = x;
   }
   SYNC();
-  PHASE(4);
+  PHASE(4); l = opaque_lane(l);
 
   // ---- phase 7: Newton solver (mj_solNewton), warm-started ----
   // per-lane rows r = l + HW * t
@@ -980,7 +994,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     if (l < NV) s.qacc[l] = use_smooth ? s.qacc_smooth[l] : s.qws[l];
   }
   SYNC();
-  PHASE(5);
+  PHASE(5); l = opaque_lane(l);
   const int cmax = wmax2(ncon);
   bool live = true;  // this env still iterating (per half)
   for (int iter = 0; iter < m.iterations; iter++) {
@@ -1043,7 +1057,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     }
     gauss = hsum(gauss, h);
     SYNC();
-    PHASE(6);
+    PHASE(6); l = opaque_lane(l);
     // Hessian rows H = M + J' D J (registers), LDL^T, search = -H^-1 grad.  Contacts that
     // touch one leg (+ base) keep H arrowhead -> tree-sparse LDL in permuted order; a contact
     // coupling two legs (either env of the wave) switches the wave to the dense factorisation.
@@ -1078,7 +1092,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
             if (sa == 3 || sb == 3) hess_acc_p<15, 18>(a, s.Jc[c], w0, w1, w2);
           }
         }
-        PHASE(14);
+        PHASE(14); l = opaque_lane(l);
         ldl_arrow(a, dinv, l, &s.x.L[0][0]);
         const float x = ldl_solve_arrow(s, a, dinv, s.grad[dn], l, h);
         if (l < NV) s.search[dn] = -x;
@@ -1106,7 +1120,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       }
     }
     SYNC();
-    PHASE(7);
+    PHASE(7); l = opaque_lane(l);
     // line-search quadratics (Gauss part) and search-direction norm
     float q1 = 0, q2 = 0, sn = 0;
     if (l < NV) {
@@ -1219,7 +1233,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
         }
       }
     }
-    PHASE(8);
+    PHASE(8); l = opaque_lane(l);
 #ifdef PP3_DEBUG
     if (blockIdx.x == 0 && h == 0) {
       if (l < NV) { g_dbg[l] = s.qacc[l]; g_dbg[18 + l] = s.grad[l]; g_dbg[36 + l] = s.search[l]; }
