@@ -342,7 +342,8 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, i
   {  // robot geoms: world position from LDS; static geoms: from the record (value select)
     const int i1 = rec.s1 >= 0 ? rec.s1 : 0, i2 = rec.s2 >= 0 ? rec.s2 : 0;
     for (int k = 0; k < 3; k++) {
-      const float l1 = s.gxpos[i1][k], l2 = s.gxpos[i2][k];
+      float l1 = s.gxpos[i1][k], l2 = s.gxpos[i2][k];
+      asm volatile("" : "+v"(l1), "+v"(l2));  // keep both loads: a pointer select would be a flat load
       p1[k] = rec.s1 >= 0 ? l1 : rec.p1[k];
       p2[k] = rec.s2 >= 0 ? l2 : rec.p2[k];
     }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# All bench configurations, one JSON line each -> gpurun_out/$1/bench_<cfg>.json
+set -e
+OUT=gpurun_out/${1:-benches}
+mkdir -p $OUT
+run() { local name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > $OUT/bench_$name.log 2>&1; tail -n 1 $OUT/bench_$name.log > $OUT/bench_$name.json; }
+run default
+run dr --dr --no-cpu-baseline
+run obst --obstacles 10 --no-cpu-baseline
+run terrain --obstacles 10 --terrain --no-cpu-baseline
+run autoreset --auto-reset 1000 --no-cpu-baseline
+run policy --policy 256,128,128 --no-cpu-baseline
+run envs8192 --envs 8192 --no-cpu-baseline
