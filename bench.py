@@ -34,14 +34,15 @@ def algorithmic_bytes_per_env_step(stride: int, H: int, dr: bool) -> int:
     return 4 * words
 
 
-def bench_kwargs(model_path):
+def bench_kwargs(model_path, random_commands=False):
     from pupperv3_mjx import config, domain_randomization
     return dict(
         path=model_path, reward_config=config.get_config(), action_scale=0.75, observation_history=2,
         joint_lower_limits=[-1.22, -0.42, -2.79, -2.51, -3.14, -0.71, -1.22, -0.42, -2.79, -2.51, -3.14, -0.71],
         joint_upper_limits=[2.51, 3.14, 0.71, 1.22, 0.42, 2.79, 2.51, 3.14, 0.71, 1.22, 0.42, 2.79],
         dof_damping=0.25, position_control_kp=5.0,
-        resample_velocity_step=2 ** 30,  # fixed command (configs[1])
+        # fixed command (configs[1]); configs[3]: the reference's default resampling every 500 steps
+        resample_velocity_step=500 if random_commands else 2 ** 30,
         maximum_pitch_command=30, maximum_roll_command=30,
         start_position_config=domain_randomization.StartPositionRandomization(
             x_min=-1.0, x_max=1.0, y_min=-1.0, y_max=1.0, z_min=0.18, z_max=0.24),
@@ -108,6 +109,8 @@ def main():
     ap.add_argument("--obstacles", type=int, default=0, help="obstacles.py boxes (configs[4])")
     ap.add_argument("--terrain", action="store_true",
                     help="per-env terrain (SURVEY 8f rank 3): every env gets its own random boxes in the --obstacles slots")
+    ap.add_argument("--random-commands", action="store_true",
+                    help="keep the reset's sampled velocity commands (configs[3]) instead of the fixed (0.5,0,0)")
     ap.add_argument("--gather", action="store_true", help="RCCL all_gather of obs|reward|done per step (configs[3])")
     ap.add_argument("--auto-reset", type=int, default=0, metavar="EPISODE_LENGTH",
                     help="on-device EpisodeWrapper+AutoResetWrapper (brax training wrap) with this episode length")
@@ -152,7 +155,7 @@ def main():
         tree.write(model_path, encoding="unicode")
 
     E = args.envs
-    env = PupperV3Env(**bench_kwargs(model_path), num_envs=E, device=device, pipeline_output=False)
+    env = PupperV3Env(**bench_kwargs(model_path, args.random_commands), num_envs=E, device=device, pipeline_output=False)
     L = env._L
     if args.dr:
         from pupperv3_mjx import domain_randomization as dr, rng
@@ -169,7 +172,8 @@ def main():
     keys = sharding.shard_keys(args.seed, E * world, world, rank)  # global env ids, contiguous shards
     st = env.reset(keys)
     rec = st._record.copy()
-    rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]
+    if not args.random_commands:
+        rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]
     env._put(_abi.F_STATE, rec)
     init_obs = st.obs.copy()
 
@@ -246,6 +250,12 @@ def main():
     rew = env._get(_abi.F_REWARD)
     obs = env._get(_abi.F_OBS)
     assert np.all(np.isfinite(rew)) and np.all(np.isfinite(obs)), "non-finite env outputs"
+    # active-contact histogram of one further (untimed) step, from the Brax-pipeline record
+    _lib.check(L.pp3_set_pipeline_output(env._h, 1))
+    env.step_device(acts.ptr.value)
+    env.synchronize()
+    ncon = env._get(_abi.F_PIPELINE)[:, _abi.P_NCON].astype(int)
+    contact_hist = np.bincount(ncon, minlength=9).tolist()
 
     if rank == 0:
         K = args.steps
@@ -274,18 +284,22 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (actions U(-1,1) pre-generated in HBM; reset keys = jax.random.split(PRNGKey(seed), E))",
-            "config": {"workload": ("configs[1]: test_pupper_model.xml, %d envs/GPU, %s, fixed command (0.5,0,0), %s"
+            "config": {"workload": ("configs[1]: test_pupper_model.xml, %d envs/GPU, %s, %s, %s"
                                     % (E, "flat terrain" if not args.obstacles else f"{args.obstacles} obstacle boxes",
+                                       "random commands" if args.random_commands else "fixed command (0.5,0,0)",
                                        "domain randomisation" if args.dr else "no DR")),
                        "envs_per_gpu": E, "global_envs": E * world, "obs_history": env._observation_history,
                        "n_frames": env._n_frames, "parallelism": f"env-sharded x{world} (no data-path collective)",
                        "per_env_terrain": bool(args.terrain),
+                       "commands": "reset-sampled, resampled every 500 steps" if args.random_commands else "fixed (0.5,0,0)",
                        "gather": bool(gather_buf is not None), "auto_reset_episode_length": args.auto_reset or None,
                        "policy_in_loop": args.policy or None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": "pp3::env_step_kernel", "bytes_per_env_step": bpe,
                          "avg_launch_ms": round(launch_s * 1e3, 4)},
+            "active_contacts": {"hist": contact_hist, "mean": round(float(np.mean(ncon)), 3),
+                                "note": "contacts per env after the run (rank 0's shard)"},
         }
         if valu:
             # Compute-side bound (DESIGN.md 'Roofline'): VALU issue.  One wave = `epw` envs; a wave64

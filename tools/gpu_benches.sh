@@ -11,3 +11,4 @@ run terrain --obstacles 10 --terrain --no-cpu-baseline
 run autoreset --auto-reset 1000 --no-cpu-baseline
 run policy --policy 256,128,128 --no-cpu-baseline
 run envs8192 --envs 8192 --no-cpu-baseline
+run c4 --envs 8192 --random-commands --no-cpu-baseline
