@@ -203,8 +203,9 @@ __device__ __forceinline__ void normalize4(float q[4]) {
   if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
   else { float i = 1.0f / n; q[0] *= i; q[1] *= i; q[2] *= i; q[3] *= i; }
 }
+// branch-free (sincos(0) = (0, 1) exactly gives mju_axisAngle2Quat's angle == 0 case); an early
+// return here made the result array a dynamically indexed private array (scratch memory)
 __device__ __forceinline__ void axisangle2quat(float r[4], const float a[3], float ang) {
-  if (ang == 0.0f) { r[0] = 1; r[1] = r[2] = r[3] = 0; return; }
   float s, c;
   sincosf(0.5f * ang, &s, &c);
   r[0] = c; r[1] = a[0] * s; r[2] = a[1] * s; r[3] = a[2] * s;
