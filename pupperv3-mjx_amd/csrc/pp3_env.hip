@@ -636,7 +636,8 @@ __device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], 
 __host__ __device__ constexpr int pnat(int p) { return p < 12 ? p + 6 : p - 12; }  // permuted -> dof
 __host__ __device__ constexpr int npos(int d) { return d < 6 ? d + 12 : d - 6; }   // dof -> permuted
 
-__device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, float* col /* >= 80 floats */) {
+__device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, float* col /* >= 80 floats */,
+                                          float (&lb)[15], float (&db)[6]) {
   l = opaque_lane(l);
   const int slot = l < NV ? l : NV;
 #pragma unroll
@@ -670,29 +671,51 @@ __device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, fl
     }
     SYNC();
   }
+  // dense 6x6 base block (the Schur complement left by the legs): ONE LDS exchange, then every
+  // lane factors it in registers (same per-element update order as row-wise elimination), so
+  // the six dependent pivot rounds cost no LDS round trips; the base rows' lanes keep their row
+  // of the factor, and every lane keeps the whole base factor for the solve (lb, db)
+  if (l >= 12 && l < NV)
 #pragma unroll
-  for (int k = 12; k < NV; ++k) {  // dense 6x6 base block
-    col[slot] = a[k];
-    SYNC();
-    float r[20];
+    for (int c = 0; c < 6; c++) col[6 * (l - 12) + c] = a[12 + c];
+  SYNC();
+  float S[6][6];
 #pragma unroll
-    for (int q = (k & ~3); q < 20; q += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(col + q);
-      r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+  for (int q = 0; q < 36; q += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(col + q);
+    S[q / 6][q % 6] = v.x; S[(q + 1) / 6][(q + 1) % 6] = v.y;
+    S[(q + 2) / 6][(q + 2) % 6] = v.z; S[(q + 3) / 6][(q + 3) % 6] = v.w;
+  }
+  SYNC();  // col is rewritten by the solve
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const float ik = frcp(fmaxf(S[k][k], MINVAL));
+    db[k] = ik;
+#pragma unroll
+    for (int i = 5; i > k; --i) {  // descending: rows below still hold their unscaled column k
+      const float lik = S[i][k] * ik;
+#pragma unroll
+      for (int j = k + 1; j <= i; ++j) S[i][j] -= lik * S[j][k];
+      S[i][k] = lik;
     }
-    const float ik = frcp(fmaxf(r[k], MINVAL));
-    dinv = (l == k) ? ik : dinv;
-    const float lik = a[k] * ik;
+  }
 #pragma unroll
-    for (int j = k + 1; j < NV; ++j) a[j] -= lik * r[j];
-    a[k] = (l > k) ? lik : a[k];
-    SYNC();
+  for (int i = 1; i < 6; ++i)
+#pragma unroll
+    for (int c = 0; c < i; ++c) lb[i * (i - 1) / 2 + c] = S[i][c];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    float v = a[12 + c];
+#pragma unroll
+    for (int i = c + 1; i < 6; ++i) v = (l == 12 + i) ? S[i][c] : v;
+    a[12 + c] = v;
+    dinv = (l == 12 + c) ? db[c] : dinv;
   }
 }
 // solve L D L^T x = b with the arrowhead factor (permuted order; lane p holds b_p on entry)
 template <int NC>
 __device__ __forceinline__ float ldl_solve_arrow(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int l,
-                                                 int h) {
+                                                 int h, const float (&lb)[15], const float (&db)[6]) {
   l = opaque_lane(l);
   const int lp = l < NV ? l : NV - 1;
   const int leg = lp < 12 ? lp / 3 : 4, li = lp - 3 * (lp < 12 ? leg : 0);  // leg index, level in leg
@@ -719,17 +742,26 @@ __device__ __forceinline__ float ldl_solve_arrow(Shared<NC>& s, const float (&a)
     for (int g = 0; g < 4; g++) t -= (l >= 12) ? a[3 * g + 2] * y[g] : 0.0f;
     x = t;
   }
+  // base block in registers on every lane (factor from ldl_arrow): forward, diagonal, backward
+  float y[6];
 #pragma unroll
-  for (int k = 12; k < NV - 1; ++k) {
-    const float yk = hb(x, k, h);
-    x = (l > k) ? x - a[k] * yk : x;
-  }
-  x = x * dinv;
+  for (int c = 0; c < 6; c++) y[c] = hb(x, 12 + c, h);
+#pragma unroll
+  for (int c = 1; c < 6; c++)
+#pragma unroll
+    for (int k = 0; k < c; k++) y[c] = y[c] - lb[c * (c - 1) / 2 + k] * y[k];
+#pragma unroll
+  for (int c = 0; c < 6; c++) y[c] = y[c] * db[c];
+#pragma unroll
+  for (int c = 4; c >= 0; --c)
+#pragma unroll
+    for (int i = 5; i > c; --i) y[c] = y[c] - lb[i * (i - 1) / 2 + c] * y[i];
+  x = x * dinv;  // leg lanes (base lanes take y below)
   SYNC();
   // backward L^T x = y: base pivots (all lanes below), then leg levels 2, 1 (own leg only)
   float colb[NV];
 #pragma unroll
-  for (int k = 12; k < NV; ++k) colb[k] = s.x.L[k][lp];
+  for (int k = 12; k < NV; ++k) colb[k] = s.x.L[k][lp];  // (used by leg lanes only)
   float cl1 = 0, cl2 = 0;  // L[leg row at level 1 / 2][lp] for lanes at lower levels of that leg
   if (lp < 12) {
     const int b0 = 3 * leg;
@@ -737,10 +769,9 @@ __device__ __forceinline__ float ldl_solve_arrow(Shared<NC>& s, const float (&a)
     cl2 = li < 2 ? s.x.L[b0 + 2][lp] : 0.0f;
   }
 #pragma unroll
-  for (int k = NV - 1; k >= 12; --k) {
-    const float xk = hb(x, k, h);
-    x = (l < k) ? x - colb[k] * xk : x;
-  }
+  for (int k = NV - 1; k >= 12; --k) x = (l < 12) ? x - colb[k] * y[k - 12] : x;
+#pragma unroll
+  for (int c = 0; c < 6; c++) x = (l == 12 + c) ? y[c] : x;
 #pragma unroll
   for (int st = 2; st > 0; --st) {
     float xs[4];
@@ -944,8 +975,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     float a[NV], dinv = 1.0f;
 #pragma unroll
     for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
-    ldl_arrow(a, dinv, l, &s.x.L[0][0]);
-    const float x = ldl_solve_arrow(s, a, dinv, s.qfrc_smooth[dn], l, h);
+    float lb[15], db[6];
+    ldl_arrow(a, dinv, l, &s.x.L[0][0], lb, db);
+    const float x = ldl_solve_arrow(s, a, dinv, s.qfrc_smooth[dn], l, h, lb, db);
     if (l < NV) s.qacc_smooth[dn] = x;
   }
   SYNC();
@@ -1094,8 +1126,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
           }
         }
         PHASE(14); l = opaque_lane(l);
-        ldl_arrow(a, dinv, l, &s.x.L[0][0]);
-        const float x = ldl_solve_arrow(s, a, dinv, s.grad[dn], l, h);
+        float lb[15], db[6];
+        ldl_arrow(a, dinv, l, &s.x.L[0][0], lb, db);
+        const float x = ldl_solve_arrow(s, a, dinv, s.grad[dn], l, h, lb, db);
         if (l < NV) s.search[dn] = -x;
       } else {
         const int li = l < NV ? l : NV - 1;
