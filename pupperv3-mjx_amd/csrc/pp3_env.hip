@@ -802,8 +802,18 @@ __device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float
   const int e = r - NFR - s.nl, c = e >> 2, ed = e & 3, t = 1 + (ed >> 1);
   const float sg = (ed & 1) ? -1.0f : 1.0f;
   float a = 0, b = 0;
+  const int sup = s.con_sup[c];
+  if (sup == 5) {  // leg-leg contact: full row
 #pragma unroll
-  for (int i = 0; i < NV; i++) { a += s.Jc[c][0][i] * x[i]; b += s.Jc[c][t][i] * x[i]; }
+    for (int i = 0; i < NV; i++) { a += s.Jc[c][0][i] * x[i]; b += s.Jc[c][t][i] * x[i]; }
+  } else {  // support = base + one leg (base-only contacts: that leg's columns are zero), in
+            // ascending column order: skipping exact zeros leaves the sum bit-identical
+#pragma unroll
+    for (int i = 0; i < 6; i++) { a += s.Jc[c][0][i] * x[i]; b += s.Jc[c][t][i] * x[i]; }
+    const int o = 6 + 3 * (sup & 3);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { a += s.Jc[c][0][o + i] * x[o + i]; b += s.Jc[c][t][o + i] * x[o + i]; }
+  }
   return a + sg * s.con_mu[c] * b;
 }
 
