@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PP3_ABI_VERSION 1
+#define PP3_ABI_VERSION 2
 
 /* ---- fixed topology of test_pupper_model.xml (checked at pp3_create) ---- */
 #define PP3_NBODY 14      /* world + base_link + 4 legs x 3 links          */
@@ -44,6 +44,8 @@ extern "C" {
 #define PP3_MAX_CGEOM 96  /* collidable geoms (8 spheres + floor + boxes)  */
 #define PP3_MAX_PAIR 640  /* candidate collision pairs after filtering     */
 #define PP3_MAX_SITE 8
+#define PP3_MAX_SENSOR 16     /* <sensor> entries (site-based types below)   */
+#define PP3_MAX_SENSORDATA 32 /* total sensordata floats                      */
 #define PP3_MAX_LAG 8     /* latency-buffer length limit                   */
 #define PP3_NREWARD 18    /* reward terms, order = PP3_REWARD_* below      */
 #define PP3_NMETRIC 19    /* total_dist + 18 scaled reward terms           */
@@ -55,6 +57,16 @@ enum { PP3_GEOM_PLANE = 0, PP3_GEOM_SPHERE = 2, PP3_GEOM_BOX = 6 };
 enum { PP3_JNT_FREE = 0, PP3_JNT_HINGE = 3 };
 enum { PP3_CONE_PYRAMIDAL = 0 };
 enum { PP3_BIAS_NONE = 0, PP3_BIAS_AFFINE = 1 };
+/* sensor types (own numbering; each is attached to a site, objtype="site") */
+enum {
+  PP3_SENS_ACCELEROMETER = 1,
+  PP3_SENS_VELOCIMETER = 2,
+  PP3_SENS_GYRO = 3,
+  PP3_SENS_FRAMEPOS = 26,
+  PP3_SENS_FRAMEQUAT = 27,
+  PP3_SENS_FRAMELINVEL = 32,
+  PP3_SENS_FRAMEANGVEL = 33
+};
 
 /* Reward-term order = the rewards_dict literal in environment.py:391-444
  * (this order is also the fp32 summation order of environment.py:446). */
@@ -155,6 +167,7 @@ typedef struct pp3_model_t {
   int32_t nsite;
   int32_t site_bodyid[PP3_MAX_SITE];
   double site_pos[PP3_MAX_SITE][3];
+  double site_quat[PP3_MAX_SITE][4];
   /* actuators (general, joint transmission) */
   int32_t actuator_trnid[PP3_NU];  /* joint id */
   int32_t actuator_biastype[PP3_NU];
@@ -168,6 +181,14 @@ typedef struct pp3_model_t {
   /* <custom> numerics (MJX collision caps; -1 = absent) */
   int32_t max_contact_points;
   int32_t max_geom_pairs;
+  /* <sensor> (xml:14-23): site sensors, sensordata = mjData.sensordata layout */
+  int32_t nsensor;
+  int32_t nsensordata;
+  int32_t sensor_type[PP3_MAX_SENSOR];   /* PP3_SENS_* */
+  int32_t sensor_objid[PP3_MAX_SENSOR];  /* site id */
+  int32_t sensor_adr[PP3_MAX_SENSOR];
+  int32_t sensor_dim[PP3_MAX_SENSOR];
+  double sensor_cutoff[PP3_MAX_SENSOR];  /* 0 = none */
 } pp3_model_t;
 
 /* Environment configuration: PupperV3Env.__init__ kwargs
@@ -269,7 +290,8 @@ enum {
   PP3_P_CON_DIST = 218,     /* 16  dist of contacts 0..15                  */
   PP3_P_CON_GEOM = 234,     /* 32  geom1, geom2 of contacts 0..15 (float)  */
   PP3_P_SUBTREE_COM = 266,  /*  3 */
-  PP3_PIPE_STRIDE = 272
+  PP3_P_SENSOR = 272,       /* 32  mjData.sensordata (model's <sensor>) */
+  PP3_PIPE_STRIDE = 304
 };
 
 /* DR record layout (domain_randomization.py:21-66, absolute values). */

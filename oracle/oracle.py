@@ -13,6 +13,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+PIPE_STRIDE = 304  # PP3_PIPE_STRIDE of include/pupper_hip.h (pipeline record incl. sensordata)
 _LIBS = {}
 
 
@@ -65,7 +66,7 @@ def mj_step(model, qpos, qvel, qacc_ws, ctrl, nsteps=1, dr=None, precision="f64"
     v = np.array(qvel, dtype=np.float64).copy()
     w = np.array(qacc_ws, dtype=np.float64).copy()
     c = np.ascontiguousarray(ctrl, dtype=np.float64)
-    pipe = np.zeros(272, dtype=np.float64) if want_pipe else None
+    pipe = np.zeros(PIPE_STRIDE, dtype=np.float64) if want_pipe else None
     sites = np.zeros((8, 3), dtype=np.float64)
     d = None if dr is None else np.ascontiguousarray(dr, dtype=np.float64)
     L.orc_boundary_take()
@@ -81,7 +82,7 @@ def mj_forward(model, qpos, qvel, qacc_ws, ctrl, precision="f64"):
     qa = np.zeros(18)
     qb = np.zeros(18)
     nefc = C.c_int()
-    pipe = np.zeros(272)
+    pipe = np.zeros(PIPE_STRIDE)
     args = [np.ascontiguousarray(x, dtype=np.float64) for x in (qpos, qvel, qacc_ws, ctrl)]
     L.orc_mj_forward(C.byref(model), *[_p(a) for a in args], _p(M), _p(qs), _p(qa), _p(qb), C.byref(nefc), _p(pipe))
     return dict(M=M, qacc_smooth=qs, qacc=qa, qfrc_bias=qb, nefc=nefc.value, pipe=pipe)
@@ -105,7 +106,7 @@ class OracleEnv:
         rew = np.zeros(1)
         done = np.zeros(1)
         met = np.zeros(19)
-        pipe = np.zeros(272)
+        pipe = np.zeros(PIPE_STRIDE)
         k = np.ascontiguousarray(key, dtype=np.uint32)
         self.L.orc_env_reset(C.byref(self.model), C.byref(self.cfg), _p(self.dr), _u(k), _p(st), _p(obs),
                              _p(rew), _p(done), _p(met), _p(pipe))
@@ -117,7 +118,7 @@ class OracleEnv:
         rew = np.zeros(1)
         done = np.zeros(1)
         met = np.zeros(19)
-        pipe = np.zeros(272)
+        pipe = np.zeros(PIPE_STRIDE)
         a = np.ascontiguousarray(action, dtype=np.float64)
         self.L.orc_boundary_take()
         self.L.orc_env_step(C.byref(self.model), C.byref(self.cfg), _p(self.dr), _p(st), _p(obs), _p(a),

@@ -271,7 +271,9 @@ typedef struct {
   real cg_solmix[PP3_MAX_CGEOM], cg_margin[PP3_MAX_CGEOM], cg_gap[PP3_MAX_CGEOM];
   int pair_g1[PP3_MAX_PAIR], pair_g2[PP3_MAX_PAIR];
   int nsite, site_body[PP3_MAX_SITE];
-  real site_pos[PP3_MAX_SITE][3];
+  real site_pos[PP3_MAX_SITE][3], site_quat[PP3_MAX_SITE][4];
+  int nsensor, sensor_type[PP3_MAX_SENSOR], sensor_objid[PP3_MAX_SENSOR], sensor_adr[PP3_MAX_SENSOR];
+  real sensor_cutoff[PP3_MAX_SENSOR];
   int act_jnt[NU], act_biastype[NU], act_forcelimited[NU], act_ctrllimited[NU];
   real act_gear[NU], act_gain[NU][3], act_bias[NU][3], act_forcerange[NU][2], act_ctrlrange[NU][2];
   int ncon_max;
@@ -303,6 +305,7 @@ typedef struct {
   real qfrc_passive[NV], qfrc_bias[NV], qfrc_actuator[NV], qfrc_smooth[NV];
   real qacc_smooth[NV], qacc[NV], qfrc_constraint[NV];
   int ls_evals; /* diagnostics */
+  real sensordata[PP3_MAX_SENSORDATA];
 } Data;
 
 static void model_from_abi(Model* M, const pp3_model_t* m, const real* dr) {
@@ -384,9 +387,17 @@ static void model_from_abi(Model* M, const pp3_model_t* m, const real* dr) {
     M->pair_g2[p] = m->pair_g2[p];
   }
   M->nsite = m->nsite;
+  M->nsensor = m->nsensor;
+  for (int i = 0; i < m->nsensor; i++) {
+    M->sensor_type[i] = m->sensor_type[i];
+    M->sensor_objid[i] = m->sensor_objid[i];
+    M->sensor_adr[i] = m->sensor_adr[i];
+    M->sensor_cutoff[i] = (real)m->sensor_cutoff[i];
+  }
   for (int s = 0; s < m->nsite; s++) {
     M->site_body[s] = m->site_bodyid[s];
     for (int k = 0; k < 3; k++) M->site_pos[s][k] = (real)m->site_pos[s][k];
+    for (int k = 0; k < 4; k++) M->site_quat[s][k] = (real)m->site_quat[s][k];
   }
   for (int a = 0; a < NU; a++) {
     M->act_jnt[a] = m->actuator_trnid[a];
@@ -1135,6 +1146,57 @@ static void solve_newton(const Model* m, Data* d) {
 }
 
 /* ================================ mj_forward / mj_step ================================ */
+/* mjData.sensordata of the last forward (mj_sensorPos/Vel/Acc for site sensors, SURVEY 8f rank
+ * 4).  Accelerations follow mj_rnePostConstraint (cacc = cacc_parent + cdof_dot.qvel + cdof.qacc,
+ * cacc_world = -gravity) and mj_objectAcceleration (transport to the site, rotate into the site
+ * frame, add the rotating-frame term omega x v); velocities follow mj_objectVelocity.  The site
+ * frame is xquat(body) * site_quat. */
+static void sensors(const Model* m, const Data* d, real* out) {
+  real cacc[NB][6];
+  for (int k = 0; k < 3; k++) { cacc[0][k] = 0; cacc[0][3 + k] = -m->gravity[k]; }
+  for (int b = 1; b < NB; b++) {
+    real t1[6] = {0, 0, 0, 0, 0, 0}, t2[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = m->dofadr[b]; i >= 0 && i < m->dofadr[b] + m->dofnum[b]; i++)
+      for (int k = 0; k < 6; k++) { t1[k] += d->cdof_dot[i][k] * d->qvel[i]; t2[k] += d->cdof[i][k] * d->qacc[i]; }
+    for (int k = 0; k < 6; k++) cacc[b][k] = cacc[m->parent[b]][k] + t1[k] + t2[k];
+  }
+  for (int i = 0; i < m->nsensor; i++) {
+    const int sid = m->sensor_objid[i], b = m->site_body[sid], typ = m->sensor_type[i];
+    real sq[4], R[9], dif[3], cr[3], vang[3], vlin[3], v[4] = {0, 0, 0, 0};
+    mulquat(sq, d->xquat[b], m->site_quat[sid]);
+    quat2mat(sq, R);
+    for (int k = 0; k < 3; k++) dif[k] = d->site_xpos[sid][k] - d->com[k];
+    for (int k = 0; k < 3; k++) vang[k] = d->cvel[b][k];
+    cross3(cr, dif, vang);
+    for (int k = 0; k < 3; k++) vlin[k] = d->cvel[b][3 + k] - cr[k];
+    int dim = 3;
+    if (typ == PP3_SENS_FRAMEPOS) for (int k = 0; k < 3; k++) v[k] = d->site_xpos[sid][k];
+    else if (typ == PP3_SENS_FRAMEQUAT) { for (int k = 0; k < 4; k++) v[k] = sq[k]; dim = 4; }
+    else if (typ == PP3_SENS_FRAMELINVEL) for (int k = 0; k < 3; k++) v[k] = vlin[k];
+    else if (typ == PP3_SENS_FRAMEANGVEL) for (int k = 0; k < 3; k++) v[k] = vang[k];
+    else if (typ == PP3_SENS_GYRO || typ == PP3_SENS_VELOCIMETER) {
+      const real* w = typ == PP3_SENS_GYRO ? vang : vlin;
+      for (int k = 0; k < 3; k++) v[k] = R[k] * w[0] + R[3 + k] * w[1] + R[6 + k] * w[2];  /* R^T w */
+    } else if (typ == PP3_SENS_ACCELEROMETER) {
+      real aang[3], alin[3], wl[3], vl[3], c2[3];
+      for (int k = 0; k < 3; k++) aang[k] = cacc[b][k];
+      cross3(cr, dif, aang);
+      for (int k = 0; k < 3; k++) alin[k] = cacc[b][3 + k] - cr[k];
+      for (int k = 0; k < 3; k++) {
+        v[k] = R[k] * alin[0] + R[3 + k] * alin[1] + R[6 + k] * alin[2];
+        wl[k] = R[k] * vang[0] + R[3 + k] * vang[1] + R[6 + k] * vang[2];
+        vl[k] = R[k] * vlin[0] + R[3 + k] * vlin[1] + R[6 + k] * vlin[2];
+      }
+      cross3(c2, wl, vl);
+      for (int k = 0; k < 3; k++) v[k] += c2[k];
+    }
+    const real co = m->sensor_cutoff[i];
+    if (co > 0 && typ != PP3_SENS_FRAMEQUAT)
+      for (int k = 0; k < 3; k++) v[k] = v[k] > co ? co : (v[k] < -co ? -co : v[k]);
+    for (int k = 0; k < dim; k++) out[m->sensor_adr[i] + k] = v[k];
+  }
+}
+
 static void forward(const Model* m, Data* d) {
   kinematics(m, d);
   com_pos(m, d);
@@ -1151,6 +1213,7 @@ static void forward(const Model* m, Data* d) {
   chol_factor(L);
   chol_solve(L, d->qacc_smooth, d->qfrc_smooth);
   solve_newton(m, d);
+  sensors(m, d, d->sensordata);  /* mj_sensorPos/Vel/Acc: before integration */
 }
 
 static void integrate(const Model* m, Data* d) {
@@ -1203,6 +1266,7 @@ static void write_pipeline(const Model* m, const Data* d, real* p) {
     p[PP3_P_CON_GEOM + 2 * c + 1] = (real)m->cg_id[d->con[c].g2];
   }
   for (int k = 0; k < 3; k++) p[PP3_P_SUBTREE_COM + k] = d->com[k];
+  for (int k = 0; k < PP3_MAX_SENSORDATA; k++) p[PP3_P_SENSOR + k] = d->sensordata[k];
 }
 
 /* ============================ exported physics API ============================ */

@@ -109,6 +109,12 @@ struct DevModel {
   int32_t nsite;
   int32_t site_body[PP3_MAX_SITE];
   float site_pos[PP3_MAX_SITE][3];
+  float site_quat[PP3_MAX_SITE][4];
+  // ---- sensors (pipeline record only) ----
+  int32_t nsensor, nsensordata;
+  int32_t sensor_type[PP3_MAX_SENSOR], sensor_objid[PP3_MAX_SENSOR], sensor_adr[PP3_MAX_SENSOR];
+  float sensor_cutoff[PP3_MAX_SENSOR];
+  int32_t body_parent[NB], body_dofadr[NB], body_dofnum[NB];
   // ---- actuators ----
   int32_t act_dof[NU], act_qadr[NU], act_biastype[NU], act_forcelimited[NU], act_ctrllimited[NU];
   float act_gear[NU], act_gain[NU], act_bias[NU][3], act_frange[NU][2], act_crange[NU][2];

@@ -1292,6 +1292,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     SYNC();
   }
   if (l < NV) s.qws[l] = s.qacc[l];
+  // the forward's velocity, kept for the sensors of the pipeline record (efc_aref is dead until
+  // the next substep rebuilds its rows)
+  if (l < NV) s.efc_aref[l] = s.qvel[l];
   SYNC();
   if (!integrate) return;
   // ---- phase 8: Euler (eulerdamp disabled) ----
@@ -1496,6 +1499,70 @@ __device__ __forceinline__ void write_obs(Shared<NC>& s, const DevModel& m, cons
   for (int k = l; k < PP3_OBS_DIM; k += HW) obs_out[k] = s.x.e.o[k];
 }
 
+// mjData.sensordata for site sensor i (lane i) from the last forward: mj_sensorPos/Vel/Acc with
+// mj_objectVelocity / mj_objectAcceleration, cacc by mj_rnePostConstraint's recursion along the
+// site body's path (oracle/pp3_oracle.c sensors() is the same restatement).  s.efc_aref holds
+// the forward's qvel (stashed before integration).
+template <int NC>
+__device__ __forceinline__ void sensor_eval(const Shared<NC>& s, const DevModel& m, int i, float* out) {
+  const int sid = m.sensor_objid[i], b = m.site_body[sid], typ = m.sensor_type[i];
+  const float* qv = s.efc_aref;
+  float xq[4] = {s.xquat[b][0], s.xquat[b][1], s.xquat[b][2], s.xquat[b][3]};
+  float Rb[9], sq[4], R[9], sx[3], off[3], dif[3], cr[3], vang[3], vlin[3], v[4] = {0, 0, 0, 0};
+  quat2mat(xq, Rb);
+  matvec(off, Rb, m.site_pos[sid]);
+  for (int k = 0; k < 3; k++) sx[k] = s.xpos[b][k] + off[k];
+  mulquat(sq, xq, m.site_quat[sid]);
+  quat2mat(sq, R);
+  for (int k = 0; k < 3; k++) { dif[k] = sx[k] - s.com[k]; vang[k] = s.cvel[b][k]; }
+  cross3(cr, dif, vang);
+  for (int k = 0; k < 3; k++) vlin[k] = s.cvel[b][3 + k] - cr[k];
+  int dim = 3;
+  if (typ == PP3_SENS_FRAMEPOS) { for (int k = 0; k < 3; k++) v[k] = sx[k]; }
+  else if (typ == PP3_SENS_FRAMEQUAT) { for (int k = 0; k < 4; k++) v[k] = sq[k]; dim = 4; }
+  else if (typ == PP3_SENS_FRAMELINVEL) { for (int k = 0; k < 3; k++) v[k] = vlin[k]; }
+  else if (typ == PP3_SENS_FRAMEANGVEL) { for (int k = 0; k < 3; k++) v[k] = vang[k]; }
+  else if (typ == PP3_SENS_GYRO || typ == PP3_SENS_VELOCIMETER) {
+    const float* w = typ == PP3_SENS_GYRO ? vang : vlin;
+    for (int k = 0; k < 3; k++) v[k] = R[k] * w[0] + R[3 + k] * w[1] + R[6 + k] * w[2];
+  } else if (typ == PP3_SENS_ACCELEROMETER) {
+    int chain[NB], n = 0;
+    for (int bb = b; bb > 0 && n < NB; bb = m.body_parent[bb]) chain[n++] = bb;
+    float ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
+    for (int c = n - 1; c >= 0; c--) {
+      const int bb = chain[c], d0 = m.body_dofadr[bb], nd = m.body_dofnum[bb];
+      float pv[6] = {0, 0, 0, 0, 0, 0};  // velocity the body's dof_dot terms see (parent, + free translation)
+      const int pb = m.body_parent[bb];
+      if (pb > 0)
+        for (int k = 0; k < 6; k++) pv[k] = s.cvel[pb][k];
+      if (nd == 6)
+        for (int d = d0; d < d0 + 3; d++)
+          for (int k = 0; k < 6; k++) pv[k] += s.cdof[d][k] * qv[d];
+      float t1[6] = {0, 0, 0, 0, 0, 0}, t2[6] = {0, 0, 0, 0, 0, 0};
+      for (int d = d0; d < d0 + nd; d++) {
+        float cdd[6] = {0, 0, 0, 0, 0, 0};
+        if (!(nd == 6 && d < d0 + 3)) cross_motion(cdd, pv, s.cdof[d]);
+        for (int k = 0; k < 6; k++) { t1[k] += cdd[k] * qv[d]; t2[k] += s.cdof[d][k] * s.qacc[d]; }
+      }
+      for (int k = 0; k < 6; k++) ca[k] = ca[k] + t1[k] + t2[k];
+    }
+    float aang[3] = {ca[0], ca[1], ca[2]}, alin[3], wl[3], vl[3], c2[3];
+    cross3(cr, dif, aang);
+    for (int k = 0; k < 3; k++) alin[k] = ca[3 + k] - cr[k];
+    for (int k = 0; k < 3; k++) {
+      v[k] = R[k] * alin[0] + R[3 + k] * alin[1] + R[6 + k] * alin[2];
+      wl[k] = R[k] * vang[0] + R[3 + k] * vang[1] + R[6 + k] * vang[2];
+      vl[k] = R[k] * vlin[0] + R[3 + k] * vlin[1] + R[6 + k] * vlin[2];
+    }
+    cross3(c2, wl, vl);
+    for (int k = 0; k < 3; k++) v[k] += c2[k];
+  }
+  const float co = m.sensor_cutoff[i];
+  if (co > 0 && typ != PP3_SENS_FRAMEQUAT)
+    for (int k = 0; k < 3; k++) v[k] = fminf(fmaxf(v[k], -co), co);
+  for (int k = 0; k < dim; k++) out[m.sensor_adr[i] + k] = v[k];
+}
+
 template <int NC>
 __device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int l) {
   for (int i = l; i < PP3_PIPE_STRIDE; i += HW) {
@@ -1518,8 +1585,10 @@ __device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m,
       const int q = i - PP3_P_CON_GEOM, c = q / 2;
       if (c < s.ncon) { const int pp = s.con_pair[c]; v = (float)m.cg_id[(q & 1) ? m.pair_g2[pp] : m.pair_g1[pp]]; }
     } else if (i < PP3_P_SUBTREE_COM + 3) v = s.com[i - PP3_P_SUBTREE_COM];
+    else if (i >= PP3_P_SENSOR && i < PP3_P_SENSOR + m.nsensordata) continue;  // written below
     p[i] = v;
   }
+  if (l < m.nsensor) sensor_eval(s, m, l, p + PP3_P_SENSOR);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2234,6 +2303,23 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
   for (int s = 0; s < mm->nsite; s++) {
     d->site_body[s] = mm->site_bodyid[s];
     for (int k = 0; k < 3; k++) d->site_pos[s][k] = (float)mm->site_pos[s][k];
+    for (int k = 0; k < 4; k++) d->site_quat[s][k] = (float)mm->site_quat[s][k];
+  }
+  if (mm->nsensor < 0 || mm->nsensor > PP3_MAX_SENSOR || mm->nsensordata > PP3_MAX_SENSORDATA)
+    return set_err(PP3_ERR_MODEL, "too many sensors");
+  d->nsensor = mm->nsensor;
+  d->nsensordata = mm->nsensordata;
+  for (int i = 0; i < mm->nsensor; i++) {
+    d->sensor_type[i] = mm->sensor_type[i];
+    d->sensor_objid[i] = mm->sensor_objid[i];
+    d->sensor_adr[i] = mm->sensor_adr[i];
+    d->sensor_cutoff[i] = (float)mm->sensor_cutoff[i];
+    if (mm->sensor_objid[i] < 0 || mm->sensor_objid[i] >= mm->nsite) return set_err(PP3_ERR_MODEL, "sensor site id");
+  }
+  for (int b = 0; b < NB; b++) {
+    d->body_parent[b] = mm->body_parentid[b];
+    d->body_dofadr[b] = mm->body_dofadr[b];
+    d->body_dofnum[b] = mm->body_dofnum[b];
   }
   for (int a = 0; a < NU; a++) {
     int j = mm->actuator_trnid[a];

@@ -5,10 +5,13 @@ tests/test_abi.py, so a drift between this file and the header fails loudly.
 """
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 NBODY, NJNT, NQ, NV, NU = 14, 13, 19, 18, 12
 NLEG, NFOOT = 4, 4
 MAX_CGEOM, MAX_PAIR, MAX_SITE, MAX_LAG = 96, 640, 8, 8
+MAX_SENSOR, MAX_SENSORDATA = 16, 32
+SENS_ACCELEROMETER, SENS_VELOCIMETER, SENS_GYRO = 1, 2, 3
+SENS_FRAMEPOS, SENS_FRAMEQUAT, SENS_FRAMELINVEL, SENS_FRAMEANGVEL = 26, 27, 32, 33
 NREWARD, NMETRIC, NDR, OBS_DIM = 18, 19, 62, 36
 
 # state record offsets (float32 words)
@@ -26,7 +29,7 @@ FIRST_STRIDE = 55
 
 P_XPOS, P_XQUAT, P_XD_VEL, P_XD_ANG = 0, 39, 91, 130
 P_SITE_XPOS, P_QFRC_ACT, P_QACC, P_NCON = 169, 181, 199, 217
-P_CON_DIST, P_CON_GEOM, P_SUBTREE_COM, PIPE_STRIDE = 218, 234, 266, 272
+P_CON_DIST, P_CON_GEOM, P_SUBTREE_COM, P_SENSOR, PIPE_STRIDE = 218, 234, 266, 272, 304
 
 DR_FRICTION, DR_KP, DR_KD, DR_BASE_IPOS, DR_INERTIA, DR_MASS = 0, 1, 2, 3, 6, 48
 
@@ -77,12 +80,16 @@ class Model(C.Structure):
         ("cgeom_gap", _a(d, MAX_CGEOM)),
         ("npair", i32), ("pair_g1", _a(i32, MAX_PAIR)), ("pair_g2", _a(i32, MAX_PAIR)),
         ("nsite", i32), ("site_bodyid", _a(i32, MAX_SITE)), ("site_pos", _a(d, MAX_SITE, 3)),
+        ("site_quat", _a(d, MAX_SITE, 4)),
         ("actuator_trnid", _a(i32, NU)), ("actuator_biastype", _a(i32, NU)),
         ("actuator_forcelimited", _a(i32, NU)), ("actuator_ctrllimited", _a(i32, NU)),
         ("actuator_gear", _a(d, NU)), ("actuator_gainprm", _a(d, NU, 3)),
         ("actuator_biasprm", _a(d, NU, 3)), ("actuator_forcerange", _a(d, NU, 2)),
         ("actuator_ctrlrange", _a(d, NU, 2)),
         ("max_contact_points", i32), ("max_geom_pairs", i32),
+        ("nsensor", i32), ("nsensordata", i32), ("sensor_type", _a(i32, MAX_SENSOR)),
+        ("sensor_objid", _a(i32, MAX_SENSOR)), ("sensor_adr", _a(i32, MAX_SENSOR)), ("sensor_dim", _a(i32, MAX_SENSOR)),
+        ("sensor_cutoff", _a(d, MAX_SENSOR)),
     ]
 
 

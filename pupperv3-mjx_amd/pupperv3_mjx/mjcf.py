@@ -141,6 +141,7 @@ class CompiledModel:
     joint_names: List[str]
     geom_names: List[str]
     site_names: List[str]
+    sensor_names: List[str]
     actuator_names: List[str]
     body_geomadr: np.ndarray
     body_geomnum: np.ndarray
@@ -249,7 +250,8 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
         for s in node.findall("site"):
             a = defaults.resolve("site", s.get("class", cls), _SITE_DEFAULTS)
             a.update(s.attrib)
-            sites.append(dict(name=a.get("name", ""), body=bid, pos=_vec(a["pos"], 3)))
+            sites.append(dict(name=a.get("name", ""), body=bid, pos=_vec(a["pos"], 3),
+                              quat=_orientation(a, angle_deg)))
             bodies[bid].sites.append(len(sites) - 1)
 
     def walk(node: ET.Element, parent: int, cls: str):
@@ -493,6 +495,7 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
     for k, s in enumerate(sites):
         m.site_bodyid[k] = s["body"]
         m.site_pos[k][:] = list(s["pos"])
+        m.site_quat[k][:] = list(s["quat"])
 
     # ---------------- actuators ----------------
     act_nodes = []
@@ -541,6 +544,40 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
             elif n.get("name") == "max_geom_pairs":
                 m.max_geom_pairs = int(float(n.get("data")))
 
+    # ---------------- sensors (site-attached types; mjData.sensordata layout) ----------------
+    sens_types = {"accelerometer": (_abi.SENS_ACCELEROMETER, 3), "velocimeter": (_abi.SENS_VELOCIMETER, 3),
+                  "gyro": (_abi.SENS_GYRO, 3), "framepos": (_abi.SENS_FRAMEPOS, 3),
+                  "framequat": (_abi.SENS_FRAMEQUAT, 4), "framelinvel": (_abi.SENS_FRAMELINVEL, 3),
+                  "frameangvel": (_abi.SENS_FRAMEANGVEL, 3)}
+    site_names = [s["name"] for s in sites]
+    m.nsensor = 0
+    m.nsensordata = 0
+    sensor_names = []
+    for sec in root.findall("sensor"):
+        for e in sec:
+            if e.tag not in sens_types:
+                raise NotImplementedError(f"sensor <{e.tag}>")
+            if e.tag.startswith("frame"):
+                if e.get("objtype") != "site" or e.get("reftype") or e.get("refname"):
+                    raise NotImplementedError(f"<{e.tag}>: only objtype=\"site\" without a reference frame")
+                site = e.get("objname")
+            else:
+                site = e.get("site")
+            if site not in site_names:
+                raise ValueError(f"sensor <{e.tag}>: unknown site {site!r}")
+            typ, dim = sens_types[e.tag]
+            k = m.nsensor
+            if k >= _abi.MAX_SENSOR or m.nsensordata + dim > _abi.MAX_SENSORDATA:
+                raise ValueError("too many sensors")
+            m.sensor_type[k] = typ
+            m.sensor_objid[k] = site_names.index(site)
+            m.sensor_adr[k] = m.nsensordata
+            m.sensor_dim[k] = dim
+            m.sensor_cutoff[k] = float(e.get("cutoff", "0"))
+            m.nsensor += 1
+            m.nsensordata += dim
+            sensor_names.append(e.get("name", f"sensor{k}"))
+
     # ---------------- set0: invweight0, meaninertia ----------------
     _set_const(m)
 
@@ -552,6 +589,7 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
         joint_names=jnames,
         geom_names=[g["name"] for g in geoms],
         site_names=[s["name"] for s in sites],
+        sensor_names=sensor_names,
         actuator_names=act_names,
         body_geomadr=body_geomadr,
         body_geomnum=body_geomnum,
