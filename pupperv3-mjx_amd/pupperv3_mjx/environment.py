@@ -59,6 +59,7 @@ class PipelineState:
     qacc: Optional[np.ndarray] = None
     contact: Optional[Contact] = None
     subtree_com: Optional[np.ndarray] = None
+    sensordata: Optional[np.ndarray] = None  # mjData.sensordata (model <sensor> order)
 
     @property
     def qpos(self):
@@ -411,6 +412,7 @@ class PupperV3Env:
             ps.contact = Contact(dist=p[:, _abi.P_CON_DIST:_abi.P_CON_DIST + 16], geom1=g[..., 0], geom2=g[..., 1])
             ps.contact.ncon = ncon
             ps.subtree_com = p[:, _abi.P_SUBTREE_COM:_abi.P_SUBTREE_COM + 3]
+            ps.sensordata = p[:, _abi.P_SENSOR:_abi.P_SENSOR + self.sys_model.struct.nsensordata]
         st = State(pipeline_state=ps, obs=obs, reward=rew, done=done, metrics=metrics, info=info)
         st._record = rec
         if single:
@@ -470,6 +472,7 @@ def _squeeze(st: State) -> State:
         ps2.qacc = sq(ps.qacc)
         ps2.contact = Contact(sq(ps.contact.dist), sq(ps.contact.geom1), sq(ps.contact.geom2))
         ps2.subtree_com = sq(ps.subtree_com)
+        ps2.sensordata = sq(ps.sensordata)
     out = State(pipeline_state=ps2, obs=sq(st.obs), reward=sq(st.reward), done=sq(st.done),
                 metrics=sq(st.metrics), info=sq(st.info))
     out._record = st._record
