@@ -2,12 +2,16 @@
 // (export.py:13-81 convert_params: dense layers, observation normalisation folded into the
 // first layer, final layer = the mean half of the Gaussian head, final activation tanh).
 //
-// One workgroup = 4 waves = a tile of 16 environments; every layer is a [16 x K] x [K x M]
-// product on the f32-input matrix cores (v_mfma_f32_16x16x4_f32: exact f32 products, f32
-// accumulation), the four waves splitting the layer's 16-column output tiles.  Activations
-// stay in LDS between layers; weights are read straight from global memory (the whole MLP
-// is a few hundred KB and stays L2-resident across workgroups).  A: lane l holds
-// X[row l&15][k0 + (l>>4)], B: W[k0 + (l>>4)][c0 + (l&15)], C/D: col l&15, row 4(l>>4)+r.
+// One workgroup = 8 waves (2 per SIMD) = a tile of 16 environments; every layer is a
+// [16 x K] x [K x M] product on the f32-input matrix cores (v_mfma_f32_16x16x4_f32: exact f32
+// products, f32 accumulation), the eight waves splitting the layer's 16-column output tiles.
+// Activations stay in LDS between layers; weights are read straight from global memory (the
+// whole MLP is a few hundred KB and stays L2-resident across workgroups) in MFMA-fragment
+// order: the host stores, per 16-column tile and group of 4 k-blocks, the 64 lanes' B values
+// as one float4 per lane, so one 16-byte load per lane (1 KB contiguous per wave) feeds four
+// MFMAs -- a row-major layout would make every MFMA's B operand a 4-row gather.  32 k-blocks
+// of a tile are in flight before its MFMAs.  A: lane l holds X[row l&15][k0 + (l>>4)],
+// B: W[k0 + (l>>4)][c0 + (l&15)], C/D: col l&15, row 4(l>>4)+r.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -20,13 +24,14 @@
 namespace pp3pol {
 
 constexpr int TILE = 16;                 // environments per workgroup
-constexpr int NWAVE = 4;
+constexpr int NWAVE = 8;
 constexpr int MAXW = PP3_POLICY_MAX_WIDTH;  // widest layer (padded)
 
 struct Layer {
-  const float* w;  // [Kp][Mp] row-major, zero padded
+  const float* w;  // fragment order [Mp/16][ngrp][64 lanes][4], zero padded
   const float* b;  // [Mp]
   int K, Kp, M, Mp, act;
+  int ngrp;  // groups of 4 k-blocks (16 inputs)
 };
 struct Net {
   Layer layer[PP3_POLICY_MAX_LAYERS];
@@ -44,6 +49,7 @@ __device__ __forceinline__ float activate(float x, int act) {
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int CG = 8;  // groups of 4 k-blocks (32 k-blocks = 128 inputs) per chunk
 
 __global__ __launch_bounds__(64 * NWAVE) void mlp_kernel(Net net, const float* __restrict__ obs, int obs_stride,
                                                          float* __restrict__ act, int act_stride, int n) {
@@ -66,41 +72,31 @@ __global__ __launch_bounds__(64 * NWAVE) void mlp_kernel(Net net, const float* _
     const bool last = li == net.n_layers - 1;
     for (int t = wave; t < ntile; t += NWAVE) {
       const int c0 = t * TILE;
-      // two independent accumulators (even / odd k blocks) cover the 40-cycle dependent MFMA
-      // latency at one wave per SIMD
+      // two independent accumulators (even / odd k blocks) cover the dependent MFMA latency
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
       const int ar = lane & 15, kk = lane >> 4;
-      const float* wc = L.w + c0 + (lane & 15);
-      // chunks of CH k blocks: all CH weight loads (L2 latency) are in flight together, then
-      // CH MFMAs run back to back on two alternating accumulators
-      constexpr int CH = 16;
-      int k0 = 0;
-      for (; k0 + 4 * CH <= L.Kp; k0 += 4 * CH) {
-        float av[CH], bv[CH];
+      const int nblk = L.Kp / 4;
+      for (int g0 = 0; g0 < L.ngrp; g0 += CG) {
+        f32x4 bq[CG];
+        float av[CG][4];
+        const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
 #pragma unroll
-        for (int q = 0; q < CH; q++) {
-          bv[q] = wc[(size_t)(k0 + 4 * q + kk) * L.Mp];
-          av[q] = X[ar][k0 + 4 * q + kk];
+        for (int q = 0; q < CG; q++) {  // every load of the chunk in flight together
+          bq[q] = (g0 + q < L.ngrp) ? wf[(size_t)q * 64] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int kb = 4 * (g0 + q) + j;
+            av[q][j] = kb < nblk ? X[ar][4 * kb + kk] : 0.0f;
+          }
         }
 #pragma unroll
-        for (int q = 0; q < CH; q += 2) {
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], acc, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q + 1], bv[q + 1], acc1, 0, 0, 0);
-        }
-      }
-      {  // tail (< CH blocks): predicated loads, same shape
-        float av[CH], bv[CH];
-#pragma unroll
-        for (int q = 0; q < CH; q++) {
-          const bool in = k0 + 4 * q < L.Kp;
-          bv[q] = in ? wc[(size_t)(k0 + 4 * q + kk) * L.Mp] : 0.0f;
-          av[q] = in ? X[ar][k0 + 4 * q + kk] : 0.0f;
-        }
-#pragma unroll
-        for (int q = 0; q < CH; q += 2) {
-          if (k0 + 4 * q >= L.Kp) break;
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], acc, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q + 1], bv[q + 1], acc1, 0, 0, 0);
+        for (int q = 0; q < CG; q++) {
+          if (g0 + q < L.ngrp) {  // uniform; padded blocks of a ragged group multiply zeros
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][0], bq[q].x, acc, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][1], bq[q].y, acc1, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][2], bq[q].z, acc, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][3], bq[q].w, acc1, 0, 0, 0);
+          }
         }
       }
       acc += acc1;
@@ -164,16 +160,24 @@ int pp3_policy_create(int32_t device, int32_t in_dim, int32_t n_layers, const in
     if (M < 1 || M > PP3_POLICY_MAX_WIDTH) return perr(PP3_ERR_ARG, "pp3_policy_create: layer width 1..576");
     if (acts[i] < PP3_ACT_LINEAR || acts[i] > PP3_ACT_SIGMOID) return perr(PP3_ERR_ARG, "pp3_policy_create: activation");
     const int Kp = (K + 3) / 4 * 4, Mp = (M + TILE - 1) / TILE * TILE;
+    const int ngrp = (Kp / 4 + 3) / 4, ntile = Mp / TILE;
     woff[i] = host.size();
-    host.resize(host.size() + (size_t)Kp * Mp, 0.0f);
-    for (int k = 0; k < K; k++)
-      for (int m = 0; m < M; m++) host[woff[i] + (size_t)k * Mp + m] = weights[src + (size_t)k * M + m];
+    host.resize(host.size() + (size_t)ntile * ngrp * 256, 0.0f);
+    for (int t = 0; t < ntile; t++)  // fragment order: [tile][group][lane][j] = W[4(4g+j) + lane/16][16t + lane%16]
+      for (int g = 0; g < ngrp; g++)
+        for (int ln = 0; ln < 64; ln++)
+          for (int j = 0; j < 4; j++) {
+            const int k = 4 * (4 * g + j) + (ln >> 4), m = TILE * t + (ln & 15);
+            if (k < K && m < M)
+              host[woff[i] + (((size_t)t * ngrp + g) * 64 + ln) * 4 + j] = weights[src + (size_t)k * M + m];
+          }
     src += (size_t)K * M;
     boff[i] = host.size();
     host.resize(host.size() + Mp, 0.0f);
     for (int m = 0; m < M; m++) host[boff[i] + m] = weights[src + m];
     src += M;
     net.layer[i].K = K; net.layer[i].Kp = Kp; net.layer[i].M = M; net.layer[i].Mp = Mp; net.layer[i].act = acts[i];
+    net.layer[i].ngrp = ngrp;
     K = M;
   }
   net.out_dim = K;
