@@ -22,6 +22,7 @@ def write_model(tmp_path, obstacles_n=0):
         xml = model_with_obstacles_xml(obstacles_n)
     else:
         xml = open(MODEL_XML).read()
+    os.makedirs(str(tmp_path), exist_ok=True)
     p = os.path.join(str(tmp_path), f"model_{obstacles_n}.xml")
     with open(p, "w") as f:
         f.write(xml)
