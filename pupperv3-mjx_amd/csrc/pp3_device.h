@@ -42,12 +42,53 @@ struct alignas(16) TerrainRec {
   float pad;
 };
 static_assert(sizeof(TerrainRec) == 64, "TerrainRec layout");
+// Contact-side constants of a candidate pair (host precomputed, 64 bytes): what store_contact
+// and the contact constraint rows read by pair index, fetched with four 16-byte loads.
+struct alignas(16) PairCon {
+  int32_t sup;       // Jacobian column support (pair_sup)
+  uint32_t dm[2];    // dof masks of the two bodies
+  float mu;          // friction (mj_contactParam)
+  float tran;        // body_invweight0 translational sum
+  float margin, b, k;
+  float solimp[5];   // clamped
+  float pad[3];
+};
+static_assert(sizeof(PairCon) == 64, "PairCon layout");
+
+// Per-lane constant records: everything lane l of one phase reads from the model, flattened on
+// the host so the lane fetches it with N back-to-back 16-byte loads at the top of the phase and
+// one vmcnt wait (lane-indexed model reads issued one by one each cost an L1/L2 round trip).
+template <int N>
+struct alignas(16) LaneRec {
+  float f[4 * N];
+};
+// phase "limits/friction/actuation": lane l < 24 = joint-limit side (j = 1 + l/2, hi side when
+// l is odd), lane l < 12 = frictionloss row of dof 6+l and actuator l
+enum {
+  LL_LIM_ON = 0, LL_RANGE, LL_MARGIN, LL_INVW, LL_B, LL_K, LL_SOLIMP,   // solimp: 5 words
+  LL_FR_R = 11, LL_FR_B, LL_ACT_DOF, LL_ACT_QADR, LL_ACT_FLAGS, LL_CRANGE,  // crange: 2 words
+  LL_GEAR = 18, LL_GAIN, LL_BIAS,  // bias: 3 words
+  LL_FRANGE = 23,                  // 2 words
+  LL_WORDS = 25
+};
+enum { ACTF_CTRLLIMITED = 1, ACTF_FORCELIMITED = 2, ACTF_AFFINE = 4 };
+// phase "com/cinert/cdof": body lanes 1..12 -> body_iquat; geom lanes (< nrobot_geom) and foot
+// lanes (16..19) -> the point's body and body-frame position
+enum { LC_IQUAT = 0, LC_PT_BODY = 4, LC_PT_POS = 5, LC_WORDS = 8 };
+// phases "M entries" / "bias" / Newton: lane l holds M pairs p = l + 32 t (t < 4) packed i | j << 8
+// (-1 = none) and their armature (i == j), dof l's damping, frictionloss of dof 6 + l
+enum { LM_IJ = 0, LM_ARM = 4, LM_DAMP = 8, LM_FLOSS = 9, LM_WORDS = 10 };
+
 constexpr float MINVAL = 1e-15f;
 constexpr float MINIMP = 0.0001f;
 constexpr float MAXIMP = 0.9999f;
 
 // fp32 model + env constants, built on the host from pp3_model_t / pp3_env_config_t.
 struct DevModel {
+  // ---- per-lane phase records (first: small offsets) ----
+  LaneRec<(LL_WORDS + 3) / 4> lane_lim[32];
+  LaneRec<(LC_WORDS + 3) / 4> lane_com[32];
+  LaneRec<(LM_WORDS + 3) / 4> lane_m[32];
   // ---- options ----
   float h;
   float gravity[3];
@@ -101,6 +142,7 @@ struct DevModel {
   int32_t pair_sup[PP3_MAX_PAIR];      // Jacobian column support: leg 0..3 (+base), 4 base only, 5 dense
   uint32_t pair_dm[PP3_MAX_PAIR][2];   // dof masks (ancestor-or-self) of the pair's two bodies
   PairRec pair_rec[PP3_MAX_PAIR];      // sphere-box: s2 = -1 - (box slot)
+  PairCon pair_con[PP3_MAX_PAIR];
   float pair_solimp[PP3_MAX_PAIR][5];  // clamped
   // per-env terrain (pp3_set_terrain): TerrainRec[N (padded even)][nbox], or 0 = static boxes
   uint64_t terrain;

@@ -105,6 +105,32 @@ struct alignas(16) Shared {
 // stop the compiler from reordering LDS accesses across them.  (__syncthreads would also
 // drain outstanding global loads, s_waitcnt vmcnt(0), and serialise the LDS queue.)
 #define SYNC() asm volatile("" ::: "memory")
+typedef float v4f __attribute__((ext_vector_type(4)));
+// Forces every listed value into a VGPR at this point: the loads feeding them are issued
+// together ahead of it and retired by one vmcnt wait, instead of each load being placed (and
+// waited for) right before its first use.
+#define PIN(...) asm volatile("" : __VA_ARGS__)
+// a lane's phase record: N 16-byte loads issued back to back, pinned together
+template <int N>
+__device__ __forceinline__ LaneRec<N> fetch_rec(const LaneRec<N>& src) {
+  const v4f* p = reinterpret_cast<const v4f*>(&src);
+  v4f v[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = p[k];
+  if constexpr (N == 1) PIN("+v"(v[0]));
+  else if constexpr (N == 2) PIN("+v"(v[0]), "+v"(v[1]));
+  else if constexpr (N == 3) PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]));
+  else if constexpr (N == 4) PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+  else if constexpr (N == 7) PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]));
+  else static_assert(N == 1, "fetch_rec: add a PIN arity");
+  LaneRec<N> r;
+#pragma unroll
+  for (int k = 0; k < N; k++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) r.f[4 * k + c] = v[k][c];
+  return r;
+}
+__device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 
 // Diagnostic build only (-DPP3_PHASE_PROF): per-phase s_memtime deltas summed over all envs.
 #ifdef PP3_PHASE_PROF
@@ -167,13 +193,34 @@ __device__ __forceinline__ int wmax2(int v) {
 // ------------------------------------------------------------------------------------
 template <int NC>
 __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l) {
+  // every model constant of the phase is fetched up front (clamped lane indices, no branches)
+  // and pinned by one asm statement: one vmcnt wait instead of one per dependent use
+  const int lc = l < 12 ? l : 11, gl = lc & 3, kl = lc >> 2;
+  const int bl = 2 + 3 * gl + kl, jl = 1 + 3 * gl + kl, ql = 7 + 3 * gl + kl;
+  float jax[3], bq[4], q0, bpos[3][3], jaxc[3][3];
+  for (int c = 0; c < 3; c++) jax[c] = m.jnt_axis[jl][c];
+  for (int c = 0; c < 4; c++) bq[c] = m.body_quat[bl][c];
+  q0 = m.qpos0[ql];
+  {
+    const int g4 = l & 3;
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        bpos[k][c] = m.body_pos[2 + 3 * g4 + k][c];
+        jaxc[k][c] = m.jnt_axis[1 + 3 * g4 + k][c];
+      }
+  }
+  PIN("+v"(jax[0]), "+v"(jax[1]), "+v"(jax[2]), "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(q0),
+      "+v"(bpos[0][0]), "+v"(bpos[0][1]), "+v"(bpos[0][2]), "+v"(bpos[1][0]), "+v"(bpos[1][1]),
+      "+v"(bpos[1][2]), "+v"(bpos[2][0]), "+v"(bpos[2][1]), "+v"(bpos[2][2]), "+v"(jaxc[0][0]),
+      "+v"(jaxc[0][1]), "+v"(jaxc[0][2]), "+v"(jaxc[1][0]), "+v"(jaxc[1][1]), "+v"(jaxc[1][2]),
+      "+v"(jaxc[2][0]), "+v"(jaxc[2][1]), "+v"(jaxc[2][2]));
   float lq[4] = {1, 0, 0, 0};
   if (l < 12) {
-    const int g = l & 3, k = l >> 2;
-    const int b = 2 + 3 * g + k, j = 1 + 3 * g + k, qa = 7 + 3 * g + k;
     float qloc[4];
-    axisangle2quat(qloc, m.jnt_axis[j], s.qpos[qa] - m.qpos0[qa]);
-    mulquat(lq, m.body_quat[b], qloc);
+    axisangle2quat(qloc, jax, s.qpos[ql] - q0);
+    mulquat(lq, bq, qloc);
   }
   // the 3 levels of this lane's leg (lanes 0..3 consume); width-32 shuffles stay in the half
   float lq1[4], lq2[4];
@@ -203,12 +250,12 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
       const int b = 2 + 3 * l + k, j = 1 + 3 * l + k;
       const float* lqk = k == 0 ? lq : (k == 1 ? lq1 : lq2);
       float xp[3], xq[4], off[3], R[9], ax[3];
-      matvec(off, pR, m.body_pos[b]);
+      matvec(off, pR, bpos[k]);
       for (int c = 0; c < 3; c++) xp[c] = pp[c] + off[c];
       mulquat(xq, pq, lqk);
       normalize4(xq);
       quat2mat(xq, R);
-      matvec(ax, R, m.jnt_axis[j]);
+      matvec(ax, R, jaxc[k]);
       matvec(off, R, s.ipos[b]);
       for (int c = 0; c < 3; c++) {
         s.xpos[b][c] = xp[c];
@@ -228,6 +275,7 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
 // ------------------------------------------------------------------------------------
 template <int NC>
 __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h) {
+  const LaneRec<2> rc = fetch_rec(m.lane_com[l]);
   const bool body = l >= 1 && l < NB;
   float mb = 0, mx = 0, my = 0, mz = 0;
   if (body) {
@@ -250,7 +298,8 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
   if (body) {
     const int b = l;
     float iq[4], R[9];
-    mulquat(iq, s.xquat[b], m.body_iquat[b]);
+    const float biq[4] = {rc.f[LC_IQUAT], rc.f[LC_IQUAT + 1], rc.f[LC_IQUAT + 2], rc.f[LC_IQUAT + 3]};
+    mulquat(iq, s.xquat[b], biq);
     quat2mat(iq, R);
     const float* I = s.inertia[b];
     float A[3][3];
@@ -304,10 +353,8 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
   // world positions of the robot collision spheres (lanes 0..7) and foot sites (16..19)
   const bool geom = l < m.nrobot_geom, foot = l >= 16 && l < 20;
   if (geom || foot) {
-    int b;
-    const float* lp;
-    if (geom) { const int g = m.robot_geom[l]; b = m.cg_body[g]; lp = m.cg_pos[g]; }
-    else { const int si = m.feet_site[l - 16]; b = m.site_body[si]; lp = m.site_pos[si]; }
+    const int b = as_i(rc.f[LC_PT_BODY]);
+    const float lp[3] = {rc.f[LC_PT_POS], rc.f[LC_PT_POS + 1], rc.f[LC_PT_POS + 2]};
     float R[9], off[3];
     quat2mat(s.xquat[b], R);
     matvec(off, R, lp);
@@ -335,8 +382,20 @@ __device__ __forceinline__ void make_frame(float f[9], const float nin[3]) {
 // the pair's flattened record (PairRec), then robot-geom world positions from LDS.
 template <int NC>
 __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, int p, float& dist, float pos[3],
-                                       float nrm[3]) {
-  const PairRec rec = m.pair_rec[p];
+                                       float nrm[3], v4f& pc0) {
+  // the pair record (6 x 16 B) and the first word group of its PairCon (for store_contact) in
+  // one batch of loads
+  PairRec rec;
+  {
+    const v4f* src = reinterpret_cast<const v4f*>(&m.pair_rec[p]);
+    v4f v[7];
+#pragma unroll
+    for (int k = 0; k < 6; k++) v[k] = src[k];
+    v[6] = *reinterpret_cast<const v4f*>(&m.pair_con[p]);
+    PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]));
+    __builtin_memcpy(&rec, v, sizeof(rec));
+    pc0 = v[6];
+  }
   const float margin = rec.margin;
   float p1[3], p2[3];
   {  // robot geoms: world position from LDS; static geoms: from the record (value select)
@@ -419,16 +478,17 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, i
 }
 
 template <int NC>
-__device__ __forceinline__ void store_contact(Shared<NC>& s, const DevModel& m, int slot, int p, float dist,
+__device__ __forceinline__ void store_contact(Shared<NC>& s, const v4f& pc0, int slot, int p, float dist,
                                               const float pos[3], const float nrm[3]) {
+  // pc0 = the pair's first PairCon word group (sup, dm[2], mu), fetched with the pair record
   s.con_pair[slot] = p;
-  s.con_sup[slot] = m.pair_sup[p];
-  s.con_dm[slot][0] = m.pair_dm[p][0];
-  s.con_dm[slot][1] = m.pair_dm[p][1];
+  s.con_sup[slot] = as_i(pc0[0]);
+  s.con_dm[slot][0] = (uint32_t)as_i(pc0[1]);
+  s.con_dm[slot][1] = (uint32_t)as_i(pc0[2]);
   s.con_dist[slot] = dist;
   for (int k = 0; k < 3; k++) s.x.a.con_pos[slot][k] = pos[k];
   make_frame(s.x.a.con_frame[slot], nrm);
-  const float mu_dr = s.fric, mu_model = m.pair_mu[p];  // values, not a pointer select (flat load)
+  const float mu_dr = s.fric, mu_model = pc0[3];
   s.con_mu[slot] = s.dr_on ? mu_dr : mu_model;
 }
 
@@ -440,11 +500,12 @@ __device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int 
   for (int base = 0; base < m.npair; base += HW) {
     const int p = base + l;
     float dist = 0, pos[3], nrm[3];
-    const bool hit = (p < m.npair) && narrow(s, m, p, dist, pos, nrm);
+    v4f pc0;
+    const bool hit = narrow(s, m, p < m.npair ? p : 0, dist, pos, nrm, pc0) && (p < m.npair);
     const uint32_t mask = hballot(hit, h);
     const int slot = nhit + __popc(mask & ((1u << l) - 1u));
     if (hit) {
-      if (slot < NC) store_contact(s, m, slot, p, dist, pos, nrm);
+      if (slot < NC) store_contact(s, pc0, slot, p, dist, pos, nrm);
       if (slot < NHIT) { s.x.a.hit_dist[slot] = dist; s.x.a.hit_pair[slot] = p; }
     }
     nhit += __popc(mask);
@@ -485,8 +546,9 @@ __device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int 
     for (int t = 0; t < NHIT / HW; t++) {
       if (keep[t]) {
         float dist, pos[3], nrm[3];
-        narrow(s, m, keep_p[t], dist, pos, nrm);
-        store_contact(s, m, slot[t], keep_p[t], dist, pos, nrm);
+        v4f pc0;
+        narrow(s, m, keep_p[t], dist, pos, nrm, pc0);
+        store_contact(s, pc0, slot[t], keep_p[t], dist, pos, nrm);
       }
     }
   }
@@ -547,7 +609,7 @@ __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m,
 #pragma unroll
     for (int k = 0; k < 10; k++) crb[k] = s.crb_base[k];
   } else {  // leg link: sum over the (<= 3) links below it in the same leg
-    const int b = m.dof_body[l], last = 2 + 3 * ((b - 2) / 3) + 2;
+    const int b = l - 4, last = 2 + 3 * ((b - 2) / 3) + 2;  // dof 6+3g+k <-> body 2+3g+k
 #pragma unroll
     for (int k = 0; k < 10; k++) crb[k] = s.cinert[b][k];
 #pragma unroll
@@ -859,16 +921,17 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   collision(s, m, l, h);
   PHASE(16); l = opaque_lane(l);
   {
+    const LaneRec<7> rl = fetch_rec(m.lane_lim[l]);
     // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
     bool act = false;
     float value = 0;
     int j = 0;
     if (l < 2 * (NJ - 1)) {
       j = 1 + (l >> 1);
-      const int side = (l & 1) ? 1 : -1;
-      if (m.jnt_limited[j]) {
-        value = side * (m.jnt_range[j][(side + 1) / 2] - s.qpos[7 + j - 1]);
-        act = value < m.lim_margin[j];
+      const float side = (l & 1) ? 1.0f : -1.0f;
+      if (as_i(rl.f[LL_LIM_ON])) {
+        value = side * (rl.f[LL_RANGE] - s.qpos[7 + j - 1]);
+        act = value < rl.f[LL_MARGIN];
       }
     }
     const uint32_t mask = hballot(act, h);
@@ -878,31 +941,31 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       const float sg = (l & 1) ? -1.0f : 1.0f;  // J = -side
       s.lim_dof[slot] = dof;
       s.lim_sgn[slot] = sg;
-      const float imp = getimp(m.lim_solimp[j], value, m.lim_margin[j]);
-      const float R = fmaxf(MINVAL, (1.0f - imp) / imp * m.lim_invw[j]);
+      const float imp = getimp(&rl.f[LL_SOLIMP], value, rl.f[LL_MARGIN]);
+      const float R = fmaxf(MINVAL, (1.0f - imp) / imp * rl.f[LL_INVW]);
       const int r = NFR + slot;
       s.efc_R[r] = R;
       s.efc_D[r] = 1.0f / R;
-      s.efc_aref[r] = -m.lim_b[j] * (sg * s.qvel[dof]) - m.lim_k[j] * imp * (value - m.lim_margin[j]);
+      s.efc_aref[r] = -rl.f[LL_B] * (sg * s.qvel[dof]) - rl.f[LL_K] * imp * (value - rl.f[LL_MARGIN]);
     }
     if (l == 0) s.nl = __popc(mask);
     if (l < NFR) {  // dof frictionloss rows (R, b precomputed: pos = 0)
       const int dof = 6 + l;
-      s.efc_R[l] = m.fr_R[dof];
-      s.efc_D[l] = 1.0f / m.fr_R[dof];
-      s.efc_aref[l] = -m.fr_b[dof] * s.qvel[dof];
+      s.efc_R[l] = rl.f[LL_FR_R];
+      s.efc_D[l] = 1.0f / rl.f[LL_FR_R];
+      s.efc_aref[l] = -rl.f[LL_FR_B] * s.qvel[dof];
     }
     if (l < NU) {  // actuation (affine PD + force clamp)
-      const int d = m.act_dof[l];
+      const int d = as_i(rl.f[LL_ACT_DOF]), flags = as_i(rl.f[LL_ACT_FLAGS]);
       float ctrl = s.ctrl[l];
-      if (m.act_ctrllimited[l]) ctrl = fminf(fmaxf(ctrl, m.act_crange[l][0]), m.act_crange[l][1]);
-      const float gear = m.act_gear[l];
-      const float len = gear * s.qpos[m.act_qadr[l]], vel = gear * s.qvel[d];
-      float gain = m.act_gain[l], b0 = m.act_bias[l][0], b1 = m.act_bias[l][1], b2 = m.act_bias[l][2];
+      if (flags & ACTF_CTRLLIMITED) ctrl = fminf(fmaxf(ctrl, rl.f[LL_CRANGE]), rl.f[LL_CRANGE + 1]);
+      const float gear = rl.f[LL_GEAR];
+      const float len = gear * s.qpos[as_i(rl.f[LL_ACT_QADR])], vel = gear * s.qvel[d];
+      float gain = rl.f[LL_GAIN], b0 = rl.f[LL_BIAS], b1 = rl.f[LL_BIAS + 1], b2 = rl.f[LL_BIAS + 2];
       if (s.dr_on) { gain = s.kp; b1 = -s.kp; b2 = -s.kd; }
       float force = gain * ctrl;
-      if (m.act_biastype[l] == PP3_BIAS_AFFINE) force += b0 + b1 * len + b2 * vel;
-      if (m.act_forcelimited[l]) force = fminf(fmaxf(force, m.act_frange[l][0]), m.act_frange[l][1]);
+      if (flags & ACTF_AFFINE) force += b0 + b1 * len + b2 * vel;
+      if (flags & ACTF_FORCELIMITED) force = fminf(fmaxf(force, rl.f[LL_FRANGE]), rl.f[LL_FRANGE + 1]);
       s.qfrc_act[d] = gear * force;
     }
     if (l < 6) s.qfrc_act[l] = 0.0f;
@@ -910,15 +973,16 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(2); l = opaque_lane(l);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
+  const LaneRec<3> rm = fetch_rec(m.lane_m[l]);  // (also read by phases 13 and 7)
 #pragma unroll
-  for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count: index loads issued up front
-    const int p = l + HW * t;
-    if (p >= NMPAIR) continue;
-    const int i = m.mp_i[p], j = m.mp_j[p];
+  for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count
+    const int ij = as_i(rm.f[LM_IJ + t]);
+    if (ij < 0) continue;
+    const int i = ij & 0xff, j = ij >> 8;
     float v = 0;
 #pragma unroll
     for (int k = 0; k < 6; k++) v += s.cdof[j][k] * s.x.a.F[i][k];
-    if (i == j) v += m.dof_armature[i];
+    v += rm.f[LM_ARM + t];  // armature on the diagonal, 0 elsewhere
     s.M[i][j] = v;
     s.M[j][i] = v;
   }
@@ -947,7 +1011,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #pragma unroll
       for (int k = 0; k < 6; k++) cf[k] = s.cfrc_base[k];
     } else {  // subtree of a leg link: itself + the (<= 2) links below (cacc holds cfrc now)
-      const int b = m.dof_body[l], last = 2 + 3 * ((b - 2) / 3) + 2;
+      const int b = l - 4, last = 2 + 3 * ((b - 2) / 3) + 2;  // dof 6+3g+k <-> body 2+3g+k (checked at create)
 #pragma unroll
       for (int k = 0; k < 6; k++) cf[k] = s.x.a.cacc[b][k];
 #pragma unroll
@@ -960,22 +1024,24 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     }
     float bias = 0;
     for (int k = 0; k < 6; k++) bias += s.cdof[l][k] * cf[k];
-    s.qfrc_smooth[l] = -m.dof_damping[l] * s.qvel[l] - bias + s.qfrc_act[l];
+    s.qfrc_smooth[l] = -rm.f[LM_DAMP] * s.qvel[l] - bias + s.qfrc_act[l];
   }
   const int nl = s.nl;
   const int nefc = NFR + nl + 4 * ncon;
   for (int e = l; e < 4 * ncon; e += HW) {
     const int c = e >> 2, p = s.con_pair[c], r = NFR + nl + e;
+    const LaneRec<4> pc = fetch_rec(*reinterpret_cast<const LaneRec<4>*>(&m.pair_con[p]));
+    const PairCon& q = *reinterpret_cast<const PairCon*>(&pc);
     const float mu = s.con_mu[c];
     const float dist = s.con_dist[c];
     const float vel = row_dot(s, r, s.qvel);
-    const float tran = m.pair_tran[p];
+    const float tran = q.tran;
     const float invw = (tran + mu * mu * tran) * 2.0f * mu * mu / m.impratio;
-    const float imp = getimp(m.pair_solimp[p], dist, m.pair_margin[p]);
+    const float imp = getimp(q.solimp, dist, q.margin);
     const float R = fmaxf(MINVAL, (1.0f - imp) / imp * invw);
     s.efc_R[r] = R;
     s.efc_D[r] = 1.0f / R;
-    s.efc_aref[r] = -m.pair_b[p] * vel - m.pair_k[p] * imp * (dist - m.pair_margin[p]);
+    s.efc_aref[r] = -q.b * vel - q.k * imp * (dist - q.margin);
   }
   SYNC();
   PHASE(13); l = opaque_lane(l);
@@ -1005,7 +1071,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     Dr[t] = valid[t] ? s.efc_D[r] : 0.0f;
     Rr[t] = valid[t] ? s.efc_R[r] : 0.0f;
     ar[t] = valid[t] ? s.efc_aref[r] : 0.0f;
-    fl[t] = (valid[t] && isfr[t]) ? m.fr_floss[6 + r] : 0.0f;
+    fl[t] = (valid[t] && isfr[t]) ? rm.f[LM_FLOSS] : 0.0f;  // row r = l (t = 0) for frictionloss rows
   }
   // warm start: total cost at qacc_warmstart vs at qacc_smooth
   float cws = 0, csm = 0;
@@ -1622,7 +1688,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   const bool own = env_raw < a.N;
   const int env = own ? env_raw : a.N - 1;
   Shared<NC>& s = sh[h];
-  const DevModel& m = *a.m;
+  const DevModel& m = *(const DevModel*)(const GModel*)a.m;  // constant AS: uniform reads -> s_load
   const int stride = m.stride;
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;
@@ -1709,7 +1775,9 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   SYNC();
   PHASE(10);
   // ---- physics: n_frames x mj_step (environment.py:366) ----
-  for (int f = 0; f < m.n_frames; f++) {
+  int n_frames = __builtin_amdgcn_readfirstlane(m.n_frames);
+  asm volatile("" : "+s"(n_frames));  // one scalar load (an invariant load is otherwise re-issued per substep)
+  for (int f = 0; f < n_frames; f++) {
     // opaque per iteration: keep model loads inside the substep (hoisting them costs more
     // registers than reloading them); the constant address space is restated after the asm so
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
@@ -1929,7 +1997,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   // envs outside N or masked out compute alongside their wave partner but store nothing
   const bool own = env_raw < a.N && (!a.mask || a.mask[env]);
   Shared<NC>& s = sh[h];
-  const DevModel& m = *a.m;
+  const DevModel& m = *(const DevModel*)(const GModel*)a.m;  // constant AS: uniform reads -> s_load
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * m.stride;
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
@@ -2008,7 +2076,7 @@ __global__ __launch_bounds__(WAVE, 2) void physics_kernel(PhysArgs a) {
   const bool own = env_raw < a.N;
   const int env = own ? env_raw : a.N - 1;
   Shared<NC>& s = sh[h];
-  const DevModel& m = *a.m;
+  const DevModel& m = *(const DevModel*)(const GModel*)a.m;  // constant AS: uniform reads -> s_load
   float* gst = a.state + (size_t)env * m.stride;
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
   if (l < NQ) s.qpos[l] = gst[PP3_S_QPOS + l];
@@ -2119,6 +2187,66 @@ static void quat2mat_d(const double q[4], double R[9]) {
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
   R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
   R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+// the per-lane phase records (pp3_device.h LaneRec) from the already filled model fields
+static void set_i(float& f, int32_t v) { memcpy(&f, &v, 4); }
+static void fill_lane_records(DevModel* d) {
+  for (int l = 0; l < 32; l++) {
+    float* f = d->lane_lim[l].f;
+    if (l < 2 * (NJ - 1)) {
+      const int j = 1 + l / 2, hi = l & 1;
+      set_i(f[LL_LIM_ON], d->jnt_limited[j] ? 1 : 0);
+      f[LL_RANGE] = d->jnt_range[j][hi];
+      f[LL_MARGIN] = d->lim_margin[j];
+      f[LL_INVW] = d->lim_invw[j];
+      f[LL_B] = d->lim_b[j];
+      f[LL_K] = d->lim_k[j];
+      for (int k = 0; k < 5; k++) f[LL_SOLIMP + k] = d->lim_solimp[j][k];
+    }
+    if (l < NFR) {
+      f[LL_FR_R] = d->fr_R[6 + l];
+      f[LL_FR_B] = d->fr_b[6 + l];
+    }
+    if (l < NU) {
+      set_i(f[LL_ACT_DOF], d->act_dof[l]);
+      set_i(f[LL_ACT_QADR], d->act_qadr[l]);
+      set_i(f[LL_ACT_FLAGS], (d->act_ctrllimited[l] ? ACTF_CTRLLIMITED : 0) | (d->act_forcelimited[l] ? ACTF_FORCELIMITED : 0) |
+                                 (d->act_biastype[l] == PP3_BIAS_AFFINE ? ACTF_AFFINE : 0));
+      f[LL_CRANGE] = d->act_crange[l][0];
+      f[LL_CRANGE + 1] = d->act_crange[l][1];
+      f[LL_GEAR] = d->act_gear[l];
+      f[LL_GAIN] = d->act_gain[l];
+      for (int k = 0; k < 3; k++) f[LL_BIAS + k] = d->act_bias[l][k];
+      f[LL_FRANGE] = d->act_frange[l][0];
+      f[LL_FRANGE + 1] = d->act_frange[l][1];
+    }
+    float* c = d->lane_com[l].f;
+    if (l >= 1 && l < NB)
+      for (int k = 0; k < 4; k++) c[LC_IQUAT + k] = d->body_iquat[l][k];
+    if (l < d->nrobot_geom) {
+      const int g = d->robot_geom[l];
+      set_i(c[LC_PT_BODY], d->cg_body[g]);
+      for (int k = 0; k < 3; k++) c[LC_PT_POS + k] = d->cg_pos[g][k];
+    } else if (l >= 16 && l < 20) {
+      const int si = d->feet_site[l - 16];
+      set_i(c[LC_PT_BODY], d->site_body[si]);
+      for (int k = 0; k < 3; k++) c[LC_PT_POS + k] = d->site_pos[si][k];
+    }
+    float* mr = d->lane_m[l].f;
+    for (int t = 0; t < 4; t++) {
+      const int p = l + 32 * t;
+      if (p < d->nmpair) {
+        const int i = d->mp_i[p], j = d->mp_j[p];
+        set_i(mr[LM_IJ + t], i | (j << 8));
+        mr[LM_ARM + t] = i == j ? d->dof_armature[i] : 0.0f;
+      } else {
+        set_i(mr[LM_IJ + t], -1);
+      }
+    }
+    if (l < NV) mr[LM_DAMP] = d->dof_damping[l];
+    if (l < NFR) mr[LM_FLOSS] = d->fr_floss[6 + l];
+  }
 }
 
 static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevModel* d) {
@@ -2297,6 +2425,19 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
       if (r.kind == PK_SPHERE_BOX)
         for (int k = 0; k < 3; k++) r.half[k] = d->cg_size[g2][k];
     }
+    {  // contact-side record
+      PairCon& q = d->pair_con[p];
+      memset(&q, 0, sizeof(q));
+      q.sup = d->pair_sup[p];
+      q.dm[0] = d->pair_dm[p][0];
+      q.dm[1] = d->pair_dm[p][1];
+      q.mu = d->pair_mu[p];
+      q.tran = d->pair_tran[p];
+      q.margin = d->pair_margin[p];
+      q.b = d->pair_b[p];
+      q.k = d->pair_k[p];
+      for (int k = 0; k < 5; k++) q.solimp[k] = d->pair_solimp[p][k];
+    }
     if (mm->cgeom_margin[g1] != 0 || mm->cgeom_margin[g2] != 0) return set_err(PP3_ERR_MODEL, "nonzero geom margins unsupported");
   }
   d->nsite = mm->nsite;
@@ -2397,6 +2538,7 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
   for (int k = 0; k < PP3_NREWARD; k++) d->scales[k] = (float)c->reward_scales[k];
   d->sigma = (float)c->tracking_sigma;
   d->pi_f = 3.14159265358979323846f;
+  fill_lane_records(d);
   return PP3_OK;
 }
 
