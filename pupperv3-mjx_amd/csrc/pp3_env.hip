@@ -1786,6 +1786,13 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     substep(s, *(const DevModel*)mp, l, h, true);
   }
   SYNC();
+  // The epilogue reads the model through a fresh opaque constant-AS pointer: after the loop's
+  // asm'd pointer, reads through the kernel-level reference are no longer proven uniform and
+  // turn into per-use vector loads (one vmcnt round trip each) instead of s_load.
+  const GModel* mq = (const GModel*)(a.m);
+  asm volatile("" : "+s"(mq));
+  {
+  const DevModel& m = *(const DevModel*)mq;
   // ---- observation (history already shifted in the prologue) ----
   get_obs(s, m, gst + m.imu_off, l, h, own, imu_stash);
   {
@@ -1965,6 +1972,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
       if (l + HW * t < PP3_S_ACT_BUF) gst[l + HW * t] = s.st[l + HW * t];
   PHASE(12);
+  }
 #ifdef PP3_PHASE_PROF
   if (l < NPROF) atomicAdd(&g_prof[l], (unsigned long long)s.prof[l]);
 #endif
