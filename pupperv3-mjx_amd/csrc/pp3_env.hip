@@ -853,6 +853,15 @@ __device__ __forceinline__ void hess_acc_p(float (&a)[NV], const float (&J)[3][N
   for (int j = J0; j < J1; j++) a[npos(j)] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
 }
 
+// row l (< NV) of M dotted with the LDS vector x, ascending j from 0
+template <int NC>
+__device__ __forceinline__ float mrow_dot(const Shared<NC>& s, int l, const float* x) {
+  float acc = 0;
+#pragma unroll
+  for (int j = 0; j < NV; j++) acc += s.M[l][j] * x[j];
+  return acc;
+}
+
 // J row r dotted with x (LDS vector)
 template <int NC>
 __device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float* x) {
@@ -869,12 +878,15 @@ __device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float
 #pragma unroll
     for (int i = 0; i < NV; i++) { a += s.Jc[c][0][i] * x[i]; b += s.Jc[c][t][i] * x[i]; }
   } else {  // support = base + one leg (base-only contacts: that leg's columns are zero), in
-            // ascending column order: skipping exact zeros leaves the sum bit-identical
-#pragma unroll
-    for (int i = 0; i < 6; i++) { a += s.Jc[c][0][i] * x[i]; b += s.Jc[c][t][i] * x[i]; }
+            // ascending column order: skipping exact zeros leaves the sum bit-identical.  (Forcing
+            // the 27 operand loads into one batch measured slower: tools/ab_bench.sh.)
     const int o = 6 + 3 * (sup & 3);
 #pragma unroll
-    for (int i = 0; i < 3; i++) { a += s.Jc[c][0][o + i] * x[o + i]; b += s.Jc[c][t][o + i] * x[o + i]; }
+    for (int i = 0; i < 9; i++) {
+      const int col = i < 6 ? i : o + i - 6;
+      a += s.Jc[c][0][col] * x[col];
+      b += s.Jc[c][t][col] * x[col];
+    }
   }
   return a + sg * s.con_mu[c] * b;
 }
@@ -1073,15 +1085,23 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     ar[t] = valid[t] ? s.efc_aref[r] : 0.0f;
     fl[t] = (valid[t] && isfr[t]) ? rm.f[LM_FLOSS] : 0.0f;  // row r = l (t = 0) for frictionloss rows
   }
-  // warm start: total cost at qacc_warmstart vs at qacc_smooth
+  // warm start: total cost at qacc_warmstart vs at qacc_smooth.  J qacc and M qacc of the first
+  // Newton iteration are one of the two candidates' products (qacc is a copy of one of them), so
+  // they are kept instead of recomputed.
   float cws = 0, csm = 0;
+  float xws[NR], xsm[NR], ma_ws = 0.0f;
+  bool use_smooth;
   {
 #pragma unroll
     for (int t = 0; t < NR; t++) {
+      xws[t] = 0.0f;
+      xsm[t] = 0.0f;
       if (!valid[t]) continue;
       const int r = l + HW * t;
       const float x1 = row_dot(s, r, s.qws) - ar[t];
       const float x2 = row_dot(s, r, s.qacc_smooth) - ar[t];
+      xws[t] = x1;
+      xsm[t] = x2;
       if (isfr[t]) {
         const float rf = Rr[t] * fl[t];
         cws += (x1 <= -rf) ? (-fl[t] * x1 - 0.5f * rf * fl[t]) : (x1 >= rf) ? (fl[t] * x1 - 0.5f * rf * fl[t]) : 0.5f * Dr[t] * x1 * x1;
@@ -1092,14 +1112,12 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       }
     }
     if (l < NV) {
-      float ma = 0;
-#pragma unroll
-      for (int j = 0; j < NV; j++) ma += s.M[l][j] * s.qws[j];
-      cws += 0.5f * (ma - s.qfrc_smooth[l]) * (s.qws[l] - s.qacc_smooth[l]);
+      ma_ws = mrow_dot(s, l, s.qws);
+      cws += 0.5f * (ma_ws - s.qfrc_smooth[l]) * (s.qws[l] - s.qacc_smooth[l]);
     }
     cws = hsum(cws, h);
     csm = hsum(csm, h);
-    const bool use_smooth = cws > csm;
+    use_smooth = cws > csm;
     if (l < NV) s.qacc[l] = use_smooth ? s.qacc_smooth[l] : s.qws[l];
   }
   SYNC();
@@ -1110,8 +1128,8 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     // Ma, Jaref, constraint state/force
     float ma = 0;
     if (l < NV) {
-#pragma unroll
-      for (int j = 0; j < NV; j++) ma += s.M[l][j] * s.qacc[j];
+      if (iter > 0 || use_smooth) ma = mrow_dot(s, l, s.qacc);
+      else ma = ma_ws;
       s.Ma[l] = ma;
     }
     float jar[NR];
@@ -1120,7 +1138,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       jar[t] = 0;
       if (!valid[t]) continue;
       const int r = l + HW * t;
-      const float x = row_dot(s, r, s.qacc) - ar[t];
+      const float x = iter > 0 ? row_dot(s, r, s.qacc) - ar[t] : (use_smooth ? xsm[t] : xws[t]);
       jar[t] = x;
       float f, Dq = 0.0f;
       if (isfr[t]) {
@@ -1235,9 +1253,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     float q1 = 0, q2 = 0, sn = 0;
     if (l < NV) {
       const float sv = s.search[l];
-      float mv = 0;
-#pragma unroll
-      for (int j = 0; j < NV; j++) mv += s.M[l][j] * s.search[j];
+      const float mv = mrow_dot(s, l, s.search);
       q1 = sv * (s.Ma[l] - s.qfrc_smooth[l]);
       q2 = 0.5f * sv * mv;
       sn = sv * sv;
