@@ -698,14 +698,32 @@ __device__ __forceinline__ float ldl_solve(Shared<NC>& s, const float (&a)[NV], 
 __host__ __device__ constexpr int pnat(int p) { return p < 12 ? p + 6 : p - 12; }  // permuted -> dof
 __host__ __device__ constexpr int npos(int d) { return d < 6 ? d + 12 : d - 6; }   // dof -> permuted
 
-__device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, float* col /* >= 80 floats */,
-                                          float (&lb)[15], float (&db)[6]) {
+__device__ __forceinline__ float dpp_shl1(float v) { return dpp_f<0x101, 0xF>(v, 0.0f); }  // lane i <- i+1 (row)
+__device__ __forceinline__ float dpp_shl2(float v) { return dpp_f<0x102, 0xF>(v, 0.0f); }  // lane i <- i+2 (row)
+
+// Factor AND solve A x = b in one pass (Gaussian elimination of the augmented rows [A | b]; A
+// symmetric positive definite, arrowhead).  Lane p holds permuted row p in a[] and b_p; returns
+// x_p.  Elimination only updates rows below the pivot, so every lane keeps its row of U (= the
+// row at the time it became pivot) and U x = y is back-substituted from registers:
+//  * 3 leg rounds (4 legs at once): each lane publishes its pivot-column entry, the pivot lane
+//    also its rhs; rows below update their entries and rhs (forward substitution fused in);
+//  * ONE exchange of the base Schur complement S and its rhs, then every lane factors and solves
+//    the 6x6 base block in registers (x_base on every lane);
+//  * leg rows back-substitute against x_base from registers and against the rows below them in
+//    the same leg through two DPP lane shifts (a leg's rows are adjacent lanes of one DPP row).
+// No transposed factor in LDS and no per-pivot lane broadcasts (cf. mj_factorM / mj_solveM).
+__device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l, float* col /* >= 80 floats */) {
   l = opaque_lane(l);
   const int slot = l < NV ? l : NV;
+  const int lp = l < NV ? l : NV - 1;
+  float dinv = 1.0f;
 #pragma unroll
   for (int st = 0; st < 3; st++) {
 #pragma unroll
-    for (int g = 0; g < 4; g++) col[20 * g + slot] = a[3 * g + st];
+    for (int g = 0; g < 4; g++) {
+      col[20 * g + slot] = a[3 * g + st];
+      if (l == 3 * g + st) col[20 * g + 19] = b;  // pivot rhs
+    }
     SYNC();
 #pragma unroll
     for (int g = 0; g < 4; g++) {
@@ -724,31 +742,36 @@ __device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, fl
       }
       const float ik = frcp(fmaxf(r[k], MINVAL));
       dinv = (l == k) ? ik : dinv;
-      const float lik = a[k] * ik;  // zero on lanes of the other legs
+      const float lik = (l > k) ? a[k] * ik : 0.0f;  // zero on rows above the pivot and other legs
 #pragma unroll
       for (int j = k + 1; j < 3 * g + 3; ++j) a[j] -= lik * r[j];
 #pragma unroll
       for (int j = 12; j < NV; ++j) a[j] -= lik * r[j];
-      a[k] = (l > k) ? lik : a[k];
+      b -= lik * r[19];
     }
     SYNC();
   }
-  // dense 6x6 base block (the Schur complement left by the legs): ONE LDS exchange, then every
-  // lane factors it in registers (same per-element update order as row-wise elimination), so
-  // the six dependent pivot rounds cost no LDS round trips; the base rows' lanes keep their row
-  // of the factor, and every lane keeps the whole base factor for the solve (lb, db)
-  if (l >= 12 && l < NV)
+  // base Schur complement and its rhs: ONE exchange; every lane then factors and solves it
+  if (l >= 12 && l < NV) {
 #pragma unroll
     for (int c = 0; c < 6; c++) col[6 * (l - 12) + c] = a[12 + c];
+    col[36 + (l - 12)] = b;
+  }
   SYNC();
-  float S[6][6];
+  float S[6][6], y[6];
 #pragma unroll
   for (int q = 0; q < 36; q += 4) {
     const float4 v = *reinterpret_cast<const float4*>(col + q);
     S[q / 6][q % 6] = v.x; S[(q + 1) / 6][(q + 1) % 6] = v.y;
     S[(q + 2) / 6][(q + 2) % 6] = v.z; S[(q + 3) / 6][(q + 3) % 6] = v.w;
   }
-  SYNC();  // col is rewritten by the solve
+  {
+    const float4 v0 = *reinterpret_cast<const float4*>(col + 36);
+    const float2 v1 = *reinterpret_cast<const float2*>(col + 40);
+    y[0] = v0.x; y[1] = v0.y; y[2] = v0.z; y[3] = v0.w; y[4] = v1.x; y[5] = v1.y;
+  }
+  SYNC();  // col is rewritten by the next use
+  float db[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     const float ik = frcp(fmaxf(S[k][k], MINVAL));
@@ -762,88 +785,31 @@ __device__ __forceinline__ void ldl_arrow(float (&a)[NV], float& dinv, int l, fl
     }
   }
 #pragma unroll
-  for (int i = 1; i < 6; ++i)
-#pragma unroll
-    for (int c = 0; c < i; ++c) lb[i * (i - 1) / 2 + c] = S[i][c];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) {
-    float v = a[12 + c];
-#pragma unroll
-    for (int i = c + 1; i < 6; ++i) v = (l == 12 + i) ? S[i][c] : v;
-    a[12 + c] = v;
-    dinv = (l == 12 + c) ? db[c] : dinv;
-  }
-}
-// solve L D L^T x = b with the arrowhead factor (permuted order; lane p holds b_p on entry)
-template <int NC>
-__device__ __forceinline__ float ldl_solve_arrow(Shared<NC>& s, const float (&a)[NV], float dinv, float x, int l,
-                                                 int h, const float (&lb)[15], const float (&db)[6]) {
-  l = opaque_lane(l);
-  const int lp = l < NV ? l : NV - 1;
-  const int leg = lp < 12 ? lp / 3 : 4, li = lp - 3 * (lp < 12 ? leg : 0);  // leg index, level in leg
-#pragma unroll
-  for (int k = 0; k < NV; ++k)
-    if (k < l && l < NV) s.x.L[l][k] = a[k];
-  // forward L y = b: three leg levels (four legs at once), then the base
-#pragma unroll
-  for (int st = 0; st < 2; st++) {
-    float y[4];
-#pragma unroll
-    for (int g = 0; g < 4; g++) y[g] = hb(x, 3 * g + st, h);
-    float t = x;
-#pragma unroll
-    for (int g = 0; g < 4; g++) t -= (l > 3 * g + st) ? a[3 * g + st] * y[g] : 0.0f;
-    x = t;
-  }
-  {
-    float y[4];
-#pragma unroll
-    for (int g = 0; g < 4; g++) y[g] = hb(x, 3 * g + 2, h);
-    float t = x;
-#pragma unroll
-    for (int g = 0; g < 4; g++) t -= (l >= 12) ? a[3 * g + 2] * y[g] : 0.0f;
-    x = t;
-  }
-  // base block in registers on every lane (factor from ldl_arrow): forward, diagonal, backward
-  float y[6];
-#pragma unroll
-  for (int c = 0; c < 6; c++) y[c] = hb(x, 12 + c, h);
-#pragma unroll
   for (int c = 1; c < 6; c++)
 #pragma unroll
-    for (int k = 0; k < c; k++) y[c] = y[c] - lb[c * (c - 1) / 2 + k] * y[k];
+    for (int k = 0; k < c; k++) y[c] = y[c] - S[c][k] * y[k];
 #pragma unroll
   for (int c = 0; c < 6; c++) y[c] = y[c] * db[c];
 #pragma unroll
   for (int c = 4; c >= 0; --c)
 #pragma unroll
-    for (int i = 5; i > c; --i) y[c] = y[c] - lb[i * (i - 1) / 2 + c] * y[i];
-  x = x * dinv;  // leg lanes (base lanes take y below)
-  SYNC();
-  // backward L^T x = y: base pivots (all lanes below), then leg levels 2, 1 (own leg only)
-  float colb[NV];
+    for (int i = 5; i > c; --i) y[c] = y[c] - S[i][c] * y[i];
+  // leg rows: U x = y from registers (base part) and the rows below in the same leg (DPP)
+  const int li = lp < 12 ? lp - 3 * (lp / 3) : 3;  // level in the leg (3 = base row)
+  float t = b;
 #pragma unroll
-  for (int k = 12; k < NV; ++k) colb[k] = s.x.L[k][lp];  // (used by leg lanes only)
-  float cl1 = 0, cl2 = 0;  // L[leg row at level 1 / 2][lp] for lanes at lower levels of that leg
-  if (lp < 12) {
-    const int b0 = 3 * leg;
-    cl1 = li < 1 ? s.x.L[b0 + 1][lp] : 0.0f;
-    cl2 = li < 2 ? s.x.L[b0 + 2][lp] : 0.0f;
-  }
+  for (int c = 0; c < 6; c++) t -= a[12 + c] * y[c];
+  // U entries to the next rows of this lane's leg: other legs' columns are exactly zero
+  const float u1 = a[1] + a[4] + a[7] + a[10], u2 = a[2] + a[5] + a[8] + a[11];
+  float x = t * dinv;                             // level 2 final
+  float v1 = dpp_shl1(x);
+  x = (li == 1) ? (t - u2 * v1) * dinv : x;       // level 1
+  v1 = dpp_shl1(x);
+  const float v2 = dpp_shl2(x);
+  x = (li == 0) ? (t - u1 * v1 - u2 * v2) * dinv : x;  // level 0
 #pragma unroll
-  for (int k = NV - 1; k >= 12; --k) x = (l < 12) ? x - colb[k] * y[k - 12] : x;
-#pragma unroll
-  for (int c = 0; c < 6; c++) x = (l == 12 + c) ? y[c] : x;
-#pragma unroll
-  for (int st = 2; st > 0; --st) {
-    float xs[4];
-#pragma unroll
-    for (int g = 0; g < 4; g++) xs[g] = hb(x, 3 * g + st, h);
-    const float xl = leg == 0 ? xs[0] : leg == 1 ? xs[1] : leg == 2 ? xs[2] : xs[3];
-    const float cv = st == 2 ? cl2 : cl1;
-    x = (lp < 12 && li < st) ? x - cv * xl : x;
-  }
-  return x;  // callers SYNC before s.x is rewritten
+  for (int c = 0; c < 6; c++) x = (lp == 12 + c) ? y[c] : x;
+  return x;
 }
 
 // a[npos(j)] += w . J[.][j] over natural columns [J0, J1) (arrowhead Hessian rows)
@@ -1060,12 +1026,14 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
   {
     const int lp = l < NV ? l : NV - 1, dn = pnat(lp);  // permuted row held by this lane
-    float a[NV], dinv = 1.0f;
+    float a[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
-    float lb[15], db[6];
-    ldl_arrow(a, dinv, l, &s.x.L[0][0], lb, db);
-    const float x = ldl_solve_arrow(s, a, dinv, s.qfrc_smooth[dn], l, h, lb, db);
+#ifdef PP3_AB_NO_LDLM  // timing ablation only: diagonal solve
+    const float x = s.qfrc_smooth[dn] / a[lp];
+#else
+    const float x = ldl_arrow_solve(a, s.qfrc_smooth[dn], l, &s.x.L[0][0]);
+#endif
     if (l < NV) s.qacc_smooth[dn] = x;
   }
   SYNC();
@@ -1196,7 +1164,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       }
       if (!dense) {
         const int lp = l < NV ? l : NV - 1, dn = pnat(lp);
-        float a[NV], dinv = 1.0f;
+        float a[NV];
 #pragma unroll
         for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
         const float dD = s.dofD[dn];
@@ -1220,9 +1188,11 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
           }
         }
         PHASE(14); l = opaque_lane(l);
-        float lb[15], db[6];
-        ldl_arrow(a, dinv, l, &s.x.L[0][0], lb, db);
-        const float x = ldl_solve_arrow(s, a, dinv, s.grad[dn], l, h, lb, db);
+#ifdef PP3_AB_NO_LDLH  // timing ablation only: diagonal solve
+        const float x = s.grad[dn] / a[lp];
+#else
+        const float x = ldl_arrow_solve(a, s.grad[dn], l, &s.x.L[0][0]);
+#endif
         if (l < NV) s.search[dn] = -x;
       } else {
         const int li = l < NV ? l : NV - 1;
@@ -1296,7 +1266,12 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     // below is per env (per half), the wave runs the union of both envs' evaluations
     float alpha = 0.0f;
     int evals = 0;
+#ifdef PP3_AB_NO_LS  // timing ablation only: full Newton step
+    alpha = live ? 1.0f : 0.0f;
+    if (false) {
+#else
     if (live) {
+#endif
       const int maxit = m.ls_iterations;
       float c0, g0, h0;
       eval(0.0f, c0, g0, h0);
@@ -1792,6 +1767,9 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   PHASE(10);
   // ---- physics: n_frames x mj_step (environment.py:366) ----
   int n_frames = __builtin_amdgcn_readfirstlane(m.n_frames);
+#ifdef PP3_AB_FRAMES
+  n_frames = PP3_AB_FRAMES;  // timing ablation only
+#endif
   asm volatile("" : "+s"(n_frames));  // one scalar load (an invariant load is otherwise re-issued per substep)
   for (int f = 0; f < n_frames; f++) {
     // opaque per iteration: keep model loads inside the substep (hoisting them costs more
@@ -1802,6 +1780,11 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     substep(s, *(const DevModel*)mp, l, h, true);
   }
   SYNC();
+#ifdef PP3_AB_NO_EPILOGUE  // timing ablation only (tools/ab_build.sh): state out, no obs/reward
+  if (own)
+    for (int t = l; t < PP3_S_ACT_BUF; t += HW) gst[t] = s.qpos[t % 20] + s.qvel[t % 18];
+  return;
+#endif
   // The epilogue reads the model through a fresh opaque constant-AS pointer: after the loop's
   // asm'd pointer, reads through the kernel-level reference are no longer proven uniform and
   // turn into per-use vector loads (one vmcnt round trip each) instead of s_load.
