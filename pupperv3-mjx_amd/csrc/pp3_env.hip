@@ -1236,24 +1236,40 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #pragma unroll
     for (int t = 0; t < NR; t++) jv[t] = valid[t] ? row_dot(s, l + HW * t, s.search) : 0.0f;
     const float gtol = m.gtol_scale * sn;
-    // cost and derivatives of the 1-D piecewise quadratic at alpha
+    // Each row's cost on the line qacc + alpha*search is piecewise quadratic in alpha: the three
+    // pieces' coefficients (below the lower switch point, above the upper one, in between) are
+    // alpha-independent and computed once here; an evaluation only picks the piece per row.
+    // Contact / limit rows: quadratic below 0, zero above; frictionloss rows: linear below -R f,
+    // linear above +R f, quadratic in between (engine_solver.c PrimalSearch cost).
+    float thr_lo[NR], thr_hi[NR], cq[NR][3], clo[NR][2], chi[NR][2];
+    bool rowany[NR];
+#pragma unroll
+    for (int t = 0; t < NR; t++) {
+      const float D = Dr[t], jr = jar[t], jw = jv[t];
+      cq[t][0] = valid[t] ? 0.5f * D * jr * jr : 0.0f;
+      cq[t][1] = valid[t] ? D * jr * jw : 0.0f;
+      cq[t][2] = valid[t] ? 0.5f * D * jw * jw : 0.0f;
+      const float rf = Rr[t] * fl[t];
+      const bool fr = valid[t] && isfr[t];
+      thr_lo[t] = fr ? -rf : -INFINITY;
+      thr_hi[t] = fr ? rf : (valid[t] ? 0.0f : INFINITY);
+      clo[t][0] = fr ? -fl[t] * jr - 0.5f * rf * fl[t] : 0.0f;
+      clo[t][1] = fr ? -fl[t] * jw : 0.0f;
+      chi[t][0] = fr ? fl[t] * jr - 0.5f * rf * fl[t] : 0.0f;
+      chi[t][1] = fr ? fl[t] * jw : 0.0f;
+      rowany[t] = __ballot(valid[t]) != 0;  // wave-uniform: skip row slots no lane uses
+    }
+    // cost and derivatives of the 1-D piecewise quadratic at alpha (alpha is per half)
     auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
       float t0 = 0, t1 = 0, t2 = 0;
 #pragma unroll
       for (int t = 0; t < NR; t++) {
-        if (!valid[t]) continue;
+        if (!rowany[t]) continue;
         const float x = jar[t] + alpha * jv[t];
-        const float D = Dr[t];
-        if (isfr[t]) {
-          const float rf = Rr[t] * fl[t];
-          if (x <= -rf) { t0 += -fl[t] * jar[t] - 0.5f * rf * fl[t]; t1 += -fl[t] * jv[t]; continue; }
-          if (x >= rf) { t0 += fl[t] * jar[t] - 0.5f * rf * fl[t]; t1 += fl[t] * jv[t]; continue; }
-        } else if (x >= 0) {
-          continue;
-        }
-        t0 += 0.5f * D * jar[t] * jar[t];
-        t1 += D * jar[t] * jv[t];
-        t2 += 0.5f * D * jv[t] * jv[t];
+        const bool lo = x <= thr_lo[t], hi = !lo && x >= thr_hi[t], qd = !lo && !hi;
+        t0 += lo ? clo[t][0] : (hi ? chi[t][0] : cq[t][0]);
+        t1 += lo ? clo[t][1] : (hi ? chi[t][1] : cq[t][1]);
+        t2 += qd ? cq[t][2] : 0.0f;
       }
       t0 = hsum(t0, h) + gauss;
       t1 = hsum(t1, h) + q1;
