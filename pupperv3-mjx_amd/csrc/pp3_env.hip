@@ -886,17 +886,20 @@ template <int NC>
 __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
   l = opaque_lane(l);
-  kinematics(s, m, l);
-  SYNC();
+  // timing ablation only (-DPP3_AB_DUP=k, tools/ab_build.sh): phase k runs twice (the phases so
+  // marked are idempotent), its cost = the time delta
+#ifndef PP3_AB_DUP
+#define PP3_AB_DUP 0
+#endif
+#define AB_REP(k) for (int ab_r_ = 0; ab_r_ < (PP3_AB_DUP == (k) ? 2 : 1); ab_r_++)
+  AB_REP(1) { kinematics(s, m, l); SYNC(); }
   PHASE(0); l = opaque_lane(l);
-  com_pos(s, m, l, h);
-  SYNC();
+  AB_REP(2) { com_pos(s, m, l, h); SYNC(); }
   PHASE(1); l = opaque_lane(l);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
-  crb_times_cdof(s, m, l);
-  rne_chain(s, m, l);
+  AB_REP(3) { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
-  collision(s, m, l, h);
+  AB_REP(4) { collision(s, m, l, h); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   {
     const LaneRec<7> rl = fetch_rec(m.lane_lim[l]);
@@ -952,6 +955,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   PHASE(2); l = opaque_lane(l);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
   const LaneRec<3> rm = fetch_rec(m.lane_m[l]);  // (also read by phases 13 and 7)
+  AB_REP(5)
 #pragma unroll
   for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count
     const int ij = as_i(rm.f[LM_IJ + t]);
@@ -983,6 +987,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(3); l = opaque_lane(l);
   // ---- phase 5: qfrc_bias/smooth (subtree sums of body forces), contact edge rows ----
+  AB_REP(12) {
   if (l < NV) {
     float cf[6];
     if (l < 6) {
@@ -1004,6 +1009,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     for (int k = 0; k < 6; k++) bias += s.cdof[l][k] * cf[k];
     s.qfrc_smooth[l] = -rm.f[LM_DAMP] * s.qvel[l] - bias + s.qfrc_act[l];
   }
+  }  // AB_REP(12): the bias part only
   const int nl = s.nl;
   const int nefc = NFR + nl + 4 * ncon;
   for (int e = l; e < 4 * ncon; e += HW) {
@@ -1024,7 +1030,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(13); l = opaque_lane(l);
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
-  {
+  AB_REP(6) {
     const int lp = l < NV ? l : NV - 1, dn = pnat(lp);  // permuted row held by this lane
     float a[NV];
 #pragma unroll
@@ -1059,7 +1065,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   float cws = 0, csm = 0;
   float xws[NR], xsm[NR], ma_ws = 0.0f;
   bool use_smooth;
-  {
+  AB_REP(8) {
 #pragma unroll
     for (int t = 0; t < NR; t++) {
       xws[t] = 0.0f;
@@ -1156,7 +1162,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     // Hessian rows H = M + J' D J (registers), LDL^T, search = -H^-1 grad.  Contacts that
     // touch one leg (+ base) keep H arrowhead -> tree-sparse LDL in permuted order; a contact
     // coupling two legs (either env of the wave) switches the wave to the dense factorisation.
-    {
+    AB_REP(10) {
       bool dense = false;
       for (int c = 0; c < cmax; c++) {
         const int sup = c < ncon ? s.con_sup[c] : 4;
