@@ -493,9 +493,11 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const v4f& pc0, int
 }
 
 // Phase 3a: collision (mj_collision), contacts compacted in pair order; when more than
-// NC pairs penetrate, the NC deepest are kept (same rule as the oracle).
+// NC pairs penetrate, the NC deepest are kept (same rule as the oracle).  Returns lane c's
+// contact support (pair_sup of contact c; 4 = no contact): the Newton phases read contact
+// supports with v_readlane from this register instead of LDS round trips per contact.
 template <int NC>
-__device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int l, int h) {
+__device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h) {
   int nhit = 0;
   for (int base = 0; base < m.npair; base += HW) {
     const int p = base + l;
@@ -552,6 +554,10 @@ __device__ __forceinline__ void collision(Shared<NC>& s, const DevModel& m, int 
       }
     }
   }
+  SYNC();
+  const int ncon_h = nhit < NC ? nhit : NC;
+  const int sup = s.con_sup[l < NC ? l : 0];
+  return l < ncon_h ? sup : 4;
 }
 
 // RNE velocity/acceleration chain (mj_comVel + forward half of mj_rne): lanes 0..3 each
@@ -899,7 +905,8 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
   AB_REP(3) { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
-  AB_REP(4) { collision(s, m, l, h); SYNC(); }
+  int lsup = 4;  // lane c: support of contact c (4 = none)
+  AB_REP(4) { lsup = collision(s, m, l, h); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   {
     const LaneRec<7> rl = fetch_rec(m.lane_lim[l]);
@@ -1163,11 +1170,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     // touch one leg (+ base) keep H arrowhead -> tree-sparse LDL in permuted order; a contact
     // coupling two legs (either env of the wave) switches the wave to the dense factorisation.
     AB_REP(10) {
-      bool dense = false;
-      for (int c = 0; c < cmax; c++) {
-        const int sup = c < ncon ? s.con_sup[c] : 4;
-        dense = dense || __builtin_amdgcn_readlane(sup, 0) == 5 || __builtin_amdgcn_readlane(sup, HW) == 5;
-      }
+      const bool dense = __ballot(lsup == 5) != 0;  // a leg-leg contact in either env
       if (!dense) {
         const int lp = l < NV ? l : NV - 1, dn = pnat(lp);
         float a[NV];
@@ -1178,8 +1181,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
         for (int j = 0; j < NV; j++) a[j] += (j == lp) ? dD : 0.0f;
         for (int c = 0; c < cmax; c++) {
           const bool cv = c < ncon;
-          const int sup = cv ? s.con_sup[c] : 4;
-          const int sa = __builtin_amdgcn_readlane(sup, 0), sb = __builtin_amdgcn_readlane(sup, HW);
+          const int sa = __builtin_amdgcn_readlane(lsup, c), sb = __builtin_amdgcn_readlane(lsup, HW + c);
           if (cv) {
             const float* G = s.con_G[c];
             const float jn = s.Jc[c][0][dn], j1 = s.Jc[c][1][dn], j2 = s.Jc[c][2][dn];
