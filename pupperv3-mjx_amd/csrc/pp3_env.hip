@@ -884,6 +884,35 @@ __device__ __forceinline__ int choice_from_uniform(const float* dist, int n, flo
   return li < n ? li : n - 1;
 }
 
+// Newton direction with a leg-leg contact (dense Hessian, rare): out of line, so its registers
+// and code do not shape the allocation and scheduling of the arrowhead path
+template <int NC>
+using LdsShared = __attribute__((address_space(3))) Shared<NC>;
+template <int NC>
+__device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l, int h, int cmax, int ncon) {
+  Shared<NC>& s = *(Shared<NC>*)sp;
+  const int li = l < NV ? l : NV - 1;
+  float a[NV], dinv = 1.0f;
+#pragma unroll
+  for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
+  const float dD = s.dofD[li];
+#pragma unroll
+  for (int j = 0; j < NV; j++) a[j] += (j == li) ? dD : 0.0f;
+  for (int c = 0; c < cmax; c++) {
+    if (c < ncon) {
+      const float* G = s.con_G[c];
+      const float jn = s.Jc[c][0][li], j1 = s.Jc[c][1][li], j2 = s.Jc[c][2][li];
+      const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
+      const float w1 = jn * G[1] + j1 * G[3];
+      const float w2 = jn * G[2] + j2 * G[4];
+      hess_acc<0, NV>(a, s.Jc[c], w0, w1, w2);
+    }
+  }
+  ldl_rows(a, dinv, l, &s.x.L[0][0]);
+  const float x = ldl_solve(s, a, dinv, s.grad[li], l, h);
+  if (l < NV) s.search[l] = -x;
+}
+
 // ------------------------------------------------------------------------------------
 // one physics substep (mj_step): forward + Newton + Euler.  `integrate` = false for reset
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
@@ -1203,26 +1232,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #endif
         if (l < NV) s.search[dn] = -x;
       } else {
-        const int li = l < NV ? l : NV - 1;
-        float a[NV], dinv = 1.0f;
-#pragma unroll
-        for (int j = 0; j < NV; j++) a[j] = s.M[li][j];
-        const float dD = s.dofD[li];
-#pragma unroll
-        for (int j = 0; j < NV; j++) a[j] += (j == li) ? dD : 0.0f;
-        for (int c = 0; c < cmax; c++) {
-          if (c < ncon) {
-            const float* G = s.con_G[c];
-            const float jn = s.Jc[c][0][li], j1 = s.Jc[c][1][li], j2 = s.Jc[c][2][li];
-            const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
-            const float w1 = jn * G[1] + j1 * G[3];
-            const float w2 = jn * G[2] + j2 * G[4];
-            hess_acc<0, NV>(a, s.Jc[c], w0, w1, w2);
-          }
-        }
-        ldl_rows(a, dinv, l, &s.x.L[0][0]);
-        const float x = ldl_solve(s, a, dinv, s.grad[li], l, h);
-        if (l < NV) s.search[l] = -x;
+        dense_search<NC>((LdsShared<NC>*)&s, l, h, cmax, ncon);
       }
     }
     SYNC();
