@@ -95,7 +95,7 @@ struct alignas(16) Shared {
   float efc_D[NEFC], efc_R[NEFC], efc_aref[NEFC], efc_force[NEFC];
   Scratch<NC> x;
 #ifdef PP3_PHASE_PROF
-  uint64_t prof[20];
+  uint64_t prof[22];
   uint64_t prof_t;
 #endif
 };
@@ -134,7 +134,7 @@ __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 
 // Diagnostic build only (-DPP3_PHASE_PROF): per-phase s_memtime deltas summed over all envs.
 #ifdef PP3_PHASE_PROF
-constexpr int NPROF = 20;
+constexpr int NPROF = 22;  // 0..18 phase cycles, 19 line-search evaluations per wave (max of its two envs), 20 per env
 __device__ unsigned long long g_prof[NPROF];
 #define PHASE(k)                                                          \
   do {                                                                    \
@@ -1368,6 +1368,12 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
         }
       }
     }
+#ifdef PP3_PHASE_PROF
+    {
+      const int ew = wmax2(evals);
+      if (l == 0) { s.prof[20] += (uint64_t)evals; if (h == 0) s.prof[19] += (uint64_t)ew; }
+    }
+#endif
     PHASE(8); l = opaque_lane(l);
 #ifdef PP3_DEBUG
     if (blockIdx.x == 0 && h == 0) {

@@ -33,15 +33,18 @@ def main():
     _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, (steps + 5) * E * 12, 1, 0, -1.0, 1.0, None))
     ms = C.c_float()
     _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, 5, C.byref(ms)))
-    buf = (C.c_uint64 * 20)()
-    _lib.check(L.pp3_phase_profile(buf, 20, 1))
+    buf = (C.c_uint64 * 22)()
+    _lib.check(L.pp3_phase_profile(buf, 22, 1))
     _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + 5 * E * 48), E * 12, steps, C.byref(ms)))
-    _lib.check(L.pp3_phase_profile(buf, 20, 1))
+    _lib.check(L.pp3_phase_profile(buf, 22, 1))
     v = np.array(buf[:len(NAMES)], dtype=np.float64)
     tot = v.sum()
     print(f"E={E}: {ms.value / steps:.3f} ms/step (prof build); cycles per env-step per env: {tot / (E * steps):.0f}")
     for n, x in zip(NAMES, v):
         print(f"  {n:32s} {100 * x / tot:6.2f}%   {x / (E * steps):10.0f} cyc/env-step")
+    nsub = steps * env.n_frames if hasattr(env, "n_frames") else steps * 5
+    print(f"  line-search evaluations per substep: {buf[20] / (E * nsub):.2f} per env, "
+          f"{buf[19] / (E / 2 * nsub):.2f} per wave (max of its two envs)")
 
 
 if __name__ == "__main__":
