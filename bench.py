@@ -309,6 +309,26 @@ def main():
                                              "ceiling_ms": round(ceil_s * 1e3, 4),
                                              "frac": round(ceil_s / launch_s, 4),
                                              "source": "profiles/traffic_r01.json (rocprofv3 SQ_INSTS_VALU)"}
+        if (world == 1 and policy is None and gather_buf is None and E == 4096 and not args.dr and not args.obstacles
+                and not args.auto_reset):
+            # Latency floor: the same step at E/2 envs puts ONE wave (two envs)
+            # on each SIMD; the kernel then takes one wave's critical path.  ratio = launch time at E
+            # / launch time at E/2 (1.0 = the second wave per SIMD is free: latency-bound).
+            half = PupperV3Env(**bench_kwargs(model_path, args.random_commands), num_envs=E // 2, device=device,
+                               pipeline_output=False)
+            hst = half.reset(keys[: E // 2])
+            hrec = hst._record.copy()
+            hrec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = rec[: E // 2, _abi.S_COMMAND:_abi.S_COMMAND + 3]
+            half._put(_abi.F_STATE, hrec)
+            _lib.check(L.pp3_step_timed(half._h, acts.ptr, E // 2 * 12, args.warmup or 5, C.byref(ms)))
+            hk = min(args.steps, 100)
+            _lib.check(L.pp3_step_timed(half._h, acts.ptr, E // 2 * 12, hk, C.byref(ms)))
+            half_s = ms.value / 1e3 / hk
+            half.close()
+            out["roofline"]["latency"] = {"envs": E // 2, "waves_per_simd": (E // 2) / 2 / N_SIMD,
+                                          "avg_launch_ms": round(half_s * 1e3, 4),
+                                          "ratio": round(launch_s / half_s, 4),
+                                          "note": "launch time at E / at E/2 envs (one wave per SIMD)"}
         if world == 1:
             out["qpos_rel_err"] = {"value": qpos_drift(env), "substeps": 1000,
                                    "vs": "fp64 oracle restatement (MuJoCo absent; parity unpinned vs mj_step)",
