@@ -118,6 +118,8 @@ def main():
                     help="policy-in-the-loop rollout: an exported-format MLP (random weights, elu) computes the "
                          "actions from the observation buffer on device before every env step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency-floor", action="store_true",
+                    help="skip the E/2-envs latency-floor launches (keeps rocprof stats to E-env launches)")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
@@ -310,7 +312,7 @@ def main():
                                              "frac": round(ceil_s / launch_s, 4),
                                              "source": "profiles/traffic_r01.json (rocprofv3 SQ_INSTS_VALU)"}
         if (world == 1 and policy is None and gather_buf is None and E == 4096 and not args.dr and not args.obstacles
-                and not args.auto_reset):
+                and not args.auto_reset and not args.no_latency_floor):
             # Latency floor: the same step at E/2 envs puts ONE wave (two envs)
             # on each SIMD; the kernel then takes one wave's critical path.  ratio = launch time at E
             # / launch time at E/2 (1.0 = the second wave per SIMD is free: latency-bound).
