@@ -862,6 +862,44 @@ __device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float
   }
   return a + sg * s.con_mu[c] * b;
 }
+// J row r dotted with two LDS vectors in one pass (the row's J entries loaded once); each result
+// is bit-identical to row_dot's
+template <int NC>
+__device__ __forceinline__ void row_dot2(const Shared<NC>& s, int r, const float* x, const float* y, float& rx,
+                                         float& ry) {
+  if (r < NFR) { rx = x[6 + r]; ry = y[6 + r]; return; }
+  if (r < NFR + s.nl) {
+    const int i = r - NFR, d = s.lim_dof[i];
+    const float sg = s.lim_sgn[i];
+    rx = sg * x[d];
+    ry = sg * y[d];
+    return;
+  }
+  const int e = r - NFR - s.nl, c = e >> 2, ed = e & 3, t = 1 + (ed >> 1);
+  const float sg = (ed & 1) ? -1.0f : 1.0f;
+  float a = 0, b = 0, a2 = 0, b2 = 0;
+  const int sup = s.con_sup[c];
+  if (sup == 5) {
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+      const float j0 = s.Jc[c][0][i], jt = s.Jc[c][t][i];
+      a += j0 * x[i]; b += jt * x[i];
+      a2 += j0 * y[i]; b2 += jt * y[i];
+    }
+  } else {
+    const int o = 6 + 3 * (sup & 3);
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int col = i < 6 ? i : o + i - 6;
+      const float j0 = s.Jc[c][0][col], jt = s.Jc[c][t][col];
+      a += j0 * x[col]; b += jt * x[col];
+      a2 += j0 * y[col]; b2 += jt * y[col];
+    }
+  }
+  const float mu = s.con_mu[c];
+  rx = a + sg * mu * b;
+  ry = a2 + sg * mu * b2;
+}
 
 // a[j] += w . J[.][j] over the columns [J0, J1) (base: 0..6, leg g: 6+3g..9+3g, dense: 0..18)
 template <int J0, int J1>
@@ -1108,8 +1146,10 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       xsm[t] = 0.0f;
       if (!valid[t]) continue;
       const int r = l + HW * t;
-      const float x1 = row_dot(s, r, s.qws) - ar[t];
-      const float x2 = row_dot(s, r, s.qacc_smooth) - ar[t];
+      float d1, d2;
+      row_dot2(s, r, s.qws, s.qacc_smooth, d1, d2);
+      const float x1 = d1 - ar[t];
+      const float x2 = d2 - ar[t];
       xws[t] = x1;
       xsm[t] = x2;
       if (isfr[t]) {
