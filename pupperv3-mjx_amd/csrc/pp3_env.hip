@@ -834,57 +834,35 @@ __device__ __forceinline__ float mrow_dot(const Shared<NC>& s, int l, const floa
   return acc;
 }
 
-// J row r dotted with x (LDS vector)
-template <int NC>
-__device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float* x) {
-  if (r < NFR) return x[6 + r];
-  if (r < NFR + s.nl) {
-    const int i = r - NFR;
-    return s.lim_sgn[i] * x[s.lim_dof[i]];
-  }
-  const int e = r - NFR - s.nl, c = e >> 2, ed = e & 3, t = 1 + (ed >> 1);
+// J row r dotted with K LDS vectors in one pass (the row's J entries loaded once).  Branch-light:
+// frictionloss rows (one dof), limit rows (one dof, signed) and pyramidal contact rows are all
+// evaluated with clamped indices and the row's value selected, instead of three divergent
+// branches per call.  Contact rows: support = base + one leg (base-only contacts: that leg's
+// columns are zero), in ascending column order, so skipping exact zeros leaves the sums
+// bit-identical; a leg-leg contact anywhere in the wave (rare) takes full rows.
+template <int NC, int K>
+__device__ __forceinline__ void row_dotk(const Shared<NC>& s, int r, const float* const (&xs)[K], float (&out)[K]) {
+  const int nl = s.nl, ncon = s.ncon;
+  const bool isf = r < NFR, isl = !isf && r < NFR + nl;
+  const int li = isl ? r - NFR : 0;
+  const int ld = s.lim_dof[li];
+  const float ls = s.lim_sgn[li];
+  const int col1 = isf ? 6 + r : (isl ? ld : 0);  // (never an uninitialised index)
+  const float sg1 = isf ? 1.0f : ls;
+  const int e0 = r - NFR - nl, e = e0 < 0 ? 0 : e0;
+  const int c = (e >> 2) < NC ? (e >> 2) : NC - 1, ed = e & 3, t = 1 + (ed >> 1);
+  const bool isc = !isf && !isl && (e0 >> 2) < ncon;
   const float sg = (ed & 1) ? -1.0f : 1.0f;
-  float a = 0, b = 0;
   const int sup = s.con_sup[c];
-  if (sup == 5) {  // leg-leg contact: full row
+  float a[K], b[K];
 #pragma unroll
-    for (int i = 0; i < NV; i++) { a += s.Jc[c][0][i] * x[i]; b += s.Jc[c][t][i] * x[i]; }
-  } else {  // support = base + one leg (base-only contacts: that leg's columns are zero), in
-            // ascending column order: skipping exact zeros leaves the sum bit-identical.  (Forcing
-            // the 27 operand loads into one batch measured slower: tools/ab_bench.sh.)
-    const int o = 6 + 3 * (sup & 3);
-#pragma unroll
-    for (int i = 0; i < 9; i++) {
-      const int col = i < 6 ? i : o + i - 6;
-      a += s.Jc[c][0][col] * x[col];
-      b += s.Jc[c][t][col] * x[col];
-    }
-  }
-  return a + sg * s.con_mu[c] * b;
-}
-// J row r dotted with two LDS vectors in one pass (the row's J entries loaded once); each result
-// is bit-identical to row_dot's
-template <int NC>
-__device__ __forceinline__ void row_dot2(const Shared<NC>& s, int r, const float* x, const float* y, float& rx,
-                                         float& ry) {
-  if (r < NFR) { rx = x[6 + r]; ry = y[6 + r]; return; }
-  if (r < NFR + s.nl) {
-    const int i = r - NFR, d = s.lim_dof[i];
-    const float sg = s.lim_sgn[i];
-    rx = sg * x[d];
-    ry = sg * y[d];
-    return;
-  }
-  const int e = r - NFR - s.nl, c = e >> 2, ed = e & 3, t = 1 + (ed >> 1);
-  const float sg = (ed & 1) ? -1.0f : 1.0f;
-  float a = 0, b = 0, a2 = 0, b2 = 0;
-  const int sup = s.con_sup[c];
-  if (sup == 5) {
+  for (int k = 0; k < K; k++) { a[k] = 0.0f; b[k] = 0.0f; }
+  if (__ballot(isc && sup == 5)) {
 #pragma unroll
     for (int i = 0; i < NV; i++) {
       const float j0 = s.Jc[c][0][i], jt = s.Jc[c][t][i];
-      a += j0 * x[i]; b += jt * x[i];
-      a2 += j0 * y[i]; b2 += jt * y[i];
+#pragma unroll
+      for (int k = 0; k < K; k++) { a[k] += j0 * xs[k][i]; b[k] += jt * xs[k][i]; }
     }
   } else {
     const int o = 6 + 3 * (sup & 3);
@@ -892,13 +870,31 @@ __device__ __forceinline__ void row_dot2(const Shared<NC>& s, int r, const float
     for (int i = 0; i < 9; i++) {
       const int col = i < 6 ? i : o + i - 6;
       const float j0 = s.Jc[c][0][col], jt = s.Jc[c][t][col];
-      a += j0 * x[col]; b += jt * x[col];
-      a2 += j0 * y[col]; b2 += jt * y[col];
+#pragma unroll
+      for (int k = 0; k < K; k++) { a[k] += j0 * xs[k][col]; b[k] += jt * xs[k][col]; }
     }
   }
   const float mu = s.con_mu[c];
-  rx = a + sg * mu * b;
-  ry = a2 + sg * mu * b2;
+#pragma unroll
+  for (int k = 0; k < K; k++) out[k] = (isf || isl) ? sg1 * xs[k][col1] : a[k] + sg * mu * b[k];
+}
+// J row r dotted with x (LDS vector)
+template <int NC>
+__device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float* x) {
+  const float* const xs[1] = {x};
+  float o[1];
+  row_dotk<NC, 1>(s, r, xs, o);
+  return o[0];
+}
+// J row r dotted with two LDS vectors in one pass
+template <int NC>
+__device__ __forceinline__ void row_dot2(const Shared<NC>& s, int r, const float* x, const float* y, float& rx,
+                                         float& ry) {
+  const float* const xs[2] = {x, y};
+  float o[2];
+  row_dotk<NC, 2>(s, r, xs, o);
+  rx = o[0];
+  ry = o[1];
 }
 
 // a[j] += w . J[.][j] over the columns [J0, J1) (base: 0..6, leg g: 6+3g..9+3g, dense: 0..18)
