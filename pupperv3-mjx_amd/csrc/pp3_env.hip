@@ -1100,11 +1100,12 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(13); l = opaque_lane(l);
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
+  float mrow[NV];  // this lane's permuted row of M, kept for the Newton Hessian (no second load)
   AB_REP(6) {
     const int lp = l < NV ? l : NV - 1, dn = pnat(lp);  // permuted row held by this lane
     float a[NV];
 #pragma unroll
-    for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
+    for (int j = 0; j < NV; j++) { a[j] = s.M[dn][pnat(j)]; mrow[j] = a[j]; }
 #ifdef PP3_AB_NO_LDLM  // timing ablation only: diagonal solve
     const float x = s.qfrc_smooth[dn] / a[lp];
 #else
@@ -1240,7 +1241,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
         const int lp = l < NV ? l : NV - 1, dn = pnat(lp);
         float a[NV];
 #pragma unroll
-        for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
+        for (int j = 0; j < NV; j++) a[j] = mrow[j];
         const float dD = s.dofD[dn];
 #pragma unroll
         for (int j = 0; j < NV; j++) a[j] += (j == lp) ? dD : 0.0f;
