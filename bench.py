@@ -103,7 +103,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=200,
+                    help="untimed steps first: the drop from the start height settles (steady state)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--dr", action="store_true", help="domain randomisation on (configs[2])")
     ap.add_argument("--obstacles", type=int, default=0, help="obstacles.py boxes (configs[4])")
