@@ -42,6 +42,35 @@ def test_substep_parity_random_states(env64, nsteps):
         np.testing.assert_array_equal(gp[:, _abi.P_NCON], op[:, _abi.P_NCON])
 
 
+@pytest.mark.parametrize("nsteps", [1, 3])
+def test_joint_limit_rows_parity(env64, nsteps):
+    """Every hinge pushed 0.02-0.2 rad past one of its limits (alternating sides): 12 active
+    limit rows per env (mj_instantiateLimit compaction, limit rows of the Newton solve and the
+    limit-row branch of the Jacobian row products), against the oracle."""
+    m = env64.sys_model.struct
+    rng_ = np.ctypeslib.as_array(m.jnt_range)[1:]
+    assert np.all(np.ctypeslib.as_array(m.jnt_limited)[1:])
+    qpos, qvel, qws, ctrl = common.random_physics_states(64, seed=20 + nsteps)
+    rs = np.random.RandomState(nsteps)
+    for i in range(64):
+        over = rs.uniform(0.02, 0.2, 12)
+        hi = (np.arange(12) + i) % 2 == 1
+        qpos[i, 7:] = np.where(hi, rng_[:, 1] + over, rng_[:, 0] - over)
+        qpos[i, 2] = 0.5  # in the air: limit rows only (no contacts)
+    qvel *= 0.1
+    gq, gv, _, gp = G.gpu_physics(env64, qpos, qvel, qws, ctrl, nsteps)
+    oq, ov, _, op = G.oracle_physics(m, qpos, qvel, qws, ctrl, nsteps)
+    fq, fv, _, _ = G.oracle_physics(m, qpos, qvel, qws, ctrl, nsteps, precision="f32")
+    assert np.all(np.isfinite(gq)) and np.all(np.isfinite(gv))
+    eq, ev = np.abs(gq - oq).max(), np.abs(gv - ov).max()
+    fq_e, fv_e = np.abs(fq - oq).max(), np.abs(fv - ov).max()
+    assert eq <= max(2e-5 * nsteps, 5 * fq_e), (eq, fq_e)
+    assert ev <= max(3e-3, 5 * fv_e), (ev, fv_e)
+    # the limits push the joints back towards their ranges
+    back = np.where((np.arange(12)[None, :] + np.arange(64)[:, None]) % 2 == 1, -1.0, 1.0)
+    assert np.mean(back * (gq[:, 7:] - qpos[:, 7:]) > 0) > 0.9
+
+
 def test_free_fall_exact(env64):
     n = 64
     qpos = np.zeros((n, 19))
