@@ -31,6 +31,7 @@ namespace pp3 {
 
 constexpr int HW = 32;      // lanes per environment (half wave)
 typedef __attribute__((address_space(4))) const DevModel GModel;  // DevModel: read-only (constant AS)
+typedef __attribute__((address_space(4))) const float GFloat;
 constexpr int HMAX = 16;    // observation_history limit
 constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + HW - 1) / HW;
 constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
@@ -905,16 +906,21 @@ __device__ __forceinline__ void hess_acc(float (&a)[NV], const float (&J)[3][NV]
 }
 
 // index drawn by jax.random.choice(p) from u = uniform(key): searchsorted_left(cumsum(p), cumsum[-1]*(1-u))
-__device__ __forceinline__ int choice_from_uniform(const float* dist, int n, float u) {
+// (n <= PP3_MAX_LAG; unrolled over the cap so the wave-uniform dist reads are one scalar load)
+__device__ __forceinline__ int choice_from_uniform(const GFloat* dist, int n, float u) {
   float total = 0.0f;
-  for (int i = 0; i < n; i++) total += dist[i];
+#pragma unroll
+  for (int i = 0; i < PP3_MAX_LAG; i++)
+    if (i < n) total += dist[i];
   const float r = total * (1.0f - u);
   float acc = 0.0f;
   int li = 0;
-  for (int i = 0; i < n; i++) {
-    acc += dist[i];
-    li += (acc < r) ? 1 : 0;
-  }
+#pragma unroll
+  for (int i = 0; i < PP3_MAX_LAG; i++)
+    if (i < n) {
+      acc += dist[i];
+      li += (acc < r) ? 1 : 0;
+    }
   return li < n ? li : n - 1;
 }
 
@@ -1551,7 +1557,7 @@ __device__ __forceinline__ void sample_orientation(const DevModel& m, Key rng, f
 // _get_obs (environment.py:485-543): consumes the st rng, pushes the IMU buffer (HBM row
 // gimu = [6][Li]), writes s.x.e.o[36]
 template <int NC>
-__device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int l, int h, bool store,
+__device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int l, int h, float pose16, bool store,
                                         const float* imu_stash = nullptr) {
   const int part = m.partitionable;
   const Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
@@ -1582,7 +1588,7 @@ __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float*
     for (int k = 0; k < 3; k++) g[k] += s.x.e.u[3 + k];
     const float gn = sqrtf(dot3(g, g));
     const float v = l < 3 ? angl[l] + s.x.e.u[l] : g[l - 3] / gn;
-    const int li = choice_from_uniform(m.imu_lat_dist, m.Li, s.x.e.u[30]);
+    const int li = choice_from_uniform((const GFloat*)m.imu_lat_dist, m.Li, s.x.e.u[30]);
     float lagged;
     if (imu_stash) {  // the row's old values were fetched at kernel start (one memory round trip)
       float old[PP3_MAX_LAG];
@@ -1605,7 +1611,7 @@ __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float*
   }
   if (l >= 16 && l < 28) {
     const int j = l - 16;
-    const float a = s.qpos[7 + j] - m.default_pose[j] + s.x.e.u[6 + j];
+    const float a = s.qpos[7 + j] - pose16 + s.x.e.u[6 + j];
     const float b = s.st[PP3_S_LAST_ACT + j] + s.x.e.u[18 + j];
     s.x.e.o[12 + j] = fminf(fmaxf(a, -100.0f), 100.0f);
     s.x.e.o[24 + j] = fminf(fmaxf(b, -100.0f), 100.0f);
@@ -1765,8 +1771,13 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (l == 0) s.prof_t = __builtin_amdgcn_s_memtime();
 #endif
   // ---- every global load of this env step issued together (one memory round trip): state
-  // record head, this lane's action-latency row and IMU row, the action, the obs history ----
+  // record head, this lane's action-latency row and IMU row, the action, the obs history, the
+  // lane's env constants and body parameters; the global stores only after all of them ----
+  int n_frames = __builtin_amdgcn_readfirstlane(m.n_frames);
   const float* act_env = a.actions + (size_t)env * NU;
+  const size_t obs_base = (size_t)env * (PP3_OBS_DIM * m.H);
+  const float* oi = a.obs_in + obs_base;
+  float* oo = a.obs_out + obs_base;
   float arow[PP3_MAX_LAG], irow[PP3_MAX_LAG], act_in = 0.0f;
   {
     const float* ar = gst + PP3_S_ACT_BUF + (l < NU ? l : 0) * m.La;
@@ -1778,32 +1789,28 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     }
     if (l < NU) act_in = act_env[l];
   }
-  {  // observation history: obs_out[36:] = obs_in[:36(H-1)] (environment.py:540-543)
-    const int nmove = PP3_OBS_DIM * (m.H - 1);
-    const float* oi = a.obs_in + (size_t)env * PP3_OBS_DIM * m.H;
-    float* oo = a.obs_out + (size_t)env * PP3_OBS_DIM * m.H;
-    float tmp[OBS_MOVE];
+  const LaneRec<2> re = m.lane_env[l];
+  // observation history: obs_out[36:] = obs_in[:36(H-1)] (environment.py:540-543)
+  const int nmove = PP3_OBS_DIM * (m.H - 1);
+  float tmp[OBS_MOVE];
 #pragma unroll
-    for (int t = 0; t < OBS_MOVE; t++) tmp[t] = (l + HW * t < nmove) ? oi[l + HW * t] : 0.0f;
-    if (own)
+  for (int t = 0; t < OBS_MOVE; t++) tmp[t] = (l + HW * t < nmove) ? oi[l + HW * t] : 0.0f;
+  float v[(PP3_S_ACT_BUF + HW - 1) / HW];  // state record head
 #pragma unroll
-      for (int t = 0; t < OBS_MOVE; t++)
-        if (l + HW * t < nmove) oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
-  }
-  {  // state record head
-    float v[(PP3_S_ACT_BUF + HW - 1) / HW];
-#pragma unroll
-    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++) v[t] = l + HW * t < PP3_S_ACT_BUF ? gst[l + HW * t] : 0.0f;
-#pragma unroll
-    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
-      if (l + HW * t < PP3_S_ACT_BUF) s.st[l + HW * t] = v[t];
-  }
+  for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++) v[t] = l + HW * t < PP3_S_ACT_BUF ? gst[l + HW * t] : 0.0f;
   // auto-reset mode: the previous step's done and this env's episode record (kept in LDS)
   if (a.episode) {
     if (l == 0) s.ep_prev_done = a.done[env];
     if (l < PP3_EP_STRIDE) s.ep[l] = a.episode[(size_t)env * PP3_EP_STRIDE + l];
   }
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
+  if (own)
+#pragma unroll
+    for (int t = 0; t < OBS_MOVE; t++)
+      if (l + HW * t < nmove) oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
+#pragma unroll
+  for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
+    if (l + HW * t < PP3_S_ACT_BUF) s.st[l + HW * t] = v[t];
   SYNC();
   if (l < NQ) s.qpos[l] = s.st[PP3_S_QPOS + l];
   if (l < NV) { s.qvel[l] = s.st[PP3_S_QVEL + l]; s.qws[l] = s.st[PP3_S_QACC_WS + l]; }
@@ -1819,7 +1826,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   }
   const float bern = hb(u, 2, h) < m.kick_p ? 1.0f : 0.0f;
   const float kick0 = hb(u, 0, h) * m.kick_vel * bern, kick1 = hb(u, 1, h) * m.kick_vel * bern;
-  const int li = choice_from_uniform(m.lat_dist, m.La, hb(u, 3, h));
+  const int li = choice_from_uniform((const GFloat*)m.lat_dist, m.La, hb(u, 3, h));
   if (l == 0) {
     s.qvel[0] += kick0;
     s.qvel[1] += kick1;
@@ -1830,8 +1837,8 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   }
   if (l < NU) {
     const float lagged = push_lagged_pre(gst + PP3_S_ACT_BUF + l * m.La, m.La, act_in, li, own, arow);
-    const float t = m.default_pose[l] + lagged * m.action_scale;
-    s.ctrl[l] = fminf(fmaxf(t, m.jlo[l]), m.jhi[l]);
+    const float t = re.f[LE_POSE] + lagged * m.action_scale;
+    s.ctrl[l] = fminf(fmaxf(t, re.f[LE_JLO]), re.f[LE_JHI]);
   }
   SYNC();
   // the state head's qpos|qvel|qacc_ws words are copied out (above) and only rewritten after the
@@ -1843,7 +1850,6 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   SYNC();
   PHASE(10);
   // ---- physics: n_frames x mj_step (environment.py:366) ----
-  int n_frames = __builtin_amdgcn_readfirstlane(m.n_frames);
 #ifdef PP3_AB_FRAMES
   n_frames = PP3_AB_FRAMES;  // timing ablation only
 #endif
@@ -1869,10 +1875,10 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   asm volatile("" : "+s"(mq));
   {
   const DevModel& m = *(const DevModel*)mq;
+  const LaneRec<2> re = fetch_rec(m.lane_env[l]);  // this lane's env constants (one round trip)
   // ---- observation (history already shifted in the prologue) ----
-  get_obs(s, m, gst + m.imu_off, l, h, own, imu_stash);
+  get_obs(s, m, gst + m.imu_off, l, h, re.f[LE_POSE16], own, imu_stash);
   {
-    float* oo = a.obs_out + (size_t)env * PP3_OBS_DIM * m.H;
     if (own)
       for (int k = l; k < PP3_OBS_DIM; k += HW) oo[k] = s.x.e.o[k];
   }
@@ -1906,7 +1912,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   const float z0[3] = {0, 0, 1};
   float ru_t[3];
   b_rotate(ru_t, z0, s.xquat[tb]);
-  const bool jviol = l < 12 && (s.qpos[7 + l] < m.jlo[l] || s.qpos[7 + l] > m.jhi[l]);
+  const bool jviol = l < 12 && (s.qpos[7 + l] < re.f[LE_JLO] || s.qpos[7 + l] > re.f[LE_JHI]);
   const bool isdone = hballot(jviol, h) != 0 || ru_t[2] < m.cos_term_angle || s.xpos[tb][2] < m.term_z;
   // ---- rewards (rewards.py) ----
   // sums over joints / dofs / feet / contacts: one element per lane, then a half-wave sum
@@ -1920,15 +1926,15 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     const float acc = (qv - s.st[PP3_S_LAST_VEL + l]) / m.env_dt;
     r_jacc = acc * acc;
     r_mech = fabsf(s.qfrc_act[6 + l] * qv);
-    const float da = act_env[l] - s.st[PP3_S_LAST_ACT + l];
+    const float da = act_in - s.st[PP3_S_LAST_ACT + l];  // act_in = action[l] (prologue load)
     r_arate = da * da;
-    r_stand = fabsf(qp - m.default_pose[l]);
+    r_stand = fabsf(qp - re.f[LE_POSE]);
     r_standv = fabsf(qv);
-    if (l % 3 == 1) { const float t = qp - m.des_abd[l / 3]; r_abd = t * t; }
+    if (l % 3 == 1) { const float t = qp - re.f[LE_ABD]; r_abd = t * t; }
   }
   if (l < 4) {
     r_air = (s.st[PP3_S_AIR_TIME + l] - 0.1f) * s.x.e.first[l];
-    const int b = m.lower_leg_body[l];
+    const int b = as_i(re.f[LE_LEG]);
     const float* sp = s.foot_xpos[l];
     const float off[3] = {sp[0] - s.xpos[b][0], sp[1] - s.xpos[b][1], sp[2] - s.xpos[b][2]};
     float cr[3];
@@ -1937,10 +1943,9 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     r_slip = (vx * vx + vy * vy) * (s.x.e.filt_cm[l] ? 1.0f : 0.0f);
   }
   if (l < s.ncon && s.con_dist[l] < 0.0f) {  // geom_collision: (contact, id) matches with dist < 0
-    const int pp = s.con_pair[l];
-    const int ga = m.cg_id[m.pair_g1[pp]], gb = m.cg_id[m.pair_g2[pp]];
-    for (int i = 0; i < m.n_knee_geoms; i++) r_knee += (ga == m.knee_geoms[i] || gb == m.knee_geoms[i]) ? 1.0f : 0.0f;
-    for (int i = 0; i < m.n_torso_geoms; i++) r_body += (ga == m.torso_geoms[i] || gb == m.torso_geoms[i]) ? 1.0f : 0.0f;
+    const v4f kb = reinterpret_cast<const v4f*>(&m.pair_con[s.con_pair[l]])[3];  // knee, body counts (host)
+    r_knee = kb[1];
+    r_body = kb[2];
   }
   r_torq = hsum(r_torq, h);
   r_jacc = hsum(r_jacc, h);
@@ -2019,7 +2024,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   }
   if (own && l < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + l] = rmine;
   if (l < NU) {
-    s.st[PP3_S_LAST_ACT + l] = act_env[l];
+    s.st[PP3_S_LAST_ACT + l] = act_in;
     s.st[PP3_S_LAST_VEL + l] = s.qvel[6 + l];
   }
   if (l < 4) {
@@ -2037,7 +2042,6 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     const float* fs = a.first_state + (size_t)env * PP3_FIRST_STRIDE;
     for (int i = l; i < PP3_FIRST_STRIDE; i += HW) s.st[PP3_S_QPOS + i] = fs[i];
     const float* fo = a.first_obs + (size_t)env * PP3_OBS_DIM * m.H;
-    float* oo = a.obs_out + (size_t)env * PP3_OBS_DIM * m.H;
     __threadfence_block();  // the prologue's history stores (other lanes, same addresses) land first
     if (own)
       for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) oo[i] = fo[i];
@@ -2123,7 +2127,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   if (own && l < m.Li) gst[m.imu_off + 5 * m.Li + l] = -1.0f;  // initial_imu_buffer gravity row
   __threadfence_block();
   __syncthreads();  // the gravity row above is global memory written by other lanes
-  get_obs(s, m, gst + m.imu_off, l, h, own);
+  get_obs(s, m, gst + m.imu_off, l, h, m.lane_env[l].f[LE_POSE16], own);
   write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, l, own);
   if (own && a.episode) {
     if (l < PP3_EP_STRIDE) a.episode[(size_t)env * PP3_EP_STRIDE + l] = 0.0f;
@@ -2330,6 +2334,23 @@ static void fill_lane_records(DevModel* d) {
     }
     if (l < NV) mr[LM_DAMP] = d->dof_damping[l];
     if (l < NFR) mr[LM_FLOSS] = d->fr_floss[6 + l];
+    float* e = d->lane_env[l].f;
+    if (l < NU) {
+      e[LE_POSE] = d->default_pose[l];
+      e[LE_JLO] = d->jlo[l];
+      e[LE_JHI] = d->jhi[l];
+      if (l % 3 == 1) e[LE_ABD] = d->des_abd[l / 3];
+    }
+    if (l < 4) set_i(e[LE_LEG], d->lower_leg_body[l]);
+    if (l >= 16 && l < 16 + NU) e[LE_POSE16] = d->default_pose[l - 16];
+  }
+  for (int p = 0; p < d->npair; p++) {
+    const int ga = d->cg_id[d->pair_g1[p]], gb = d->cg_id[d->pair_g2[p]];
+    int kn = 0, bo = 0;
+    for (int i = 0; i < d->n_knee_geoms; i++) kn += (ga == d->knee_geoms[i] || gb == d->knee_geoms[i]) ? 1 : 0;
+    for (int i = 0; i < d->n_torso_geoms; i++) bo += (ga == d->torso_geoms[i] || gb == d->torso_geoms[i]) ? 1 : 0;
+    d->pair_con[p].knee = (float)kn;
+    d->pair_con[p].body = (float)bo;
   }
 }
 
