@@ -64,6 +64,13 @@ template <int N>
 struct alignas(16) LaneRec {
   float f[4 * N];
 };
+// The model stores a phase's 32 lane records word-group major (group k of lane l at g[k][l]):
+// the wave's k-th 16-byte load then covers 512 contiguous bytes (4 cache lines) instead of
+// 16-byte pieces of 32 records strided across up to 32 lines.
+template <int N>
+struct alignas(16) LaneTab {
+  float g[N][32][4];
+};
 // phase "limits/friction/actuation": lane l < 24 = joint-limit side (j = 1 + l/2, hi side when
 // l is odd), lane l < 12 = frictionloss row of dof 6+l and actuator l
 enum {
@@ -92,9 +99,9 @@ constexpr float MAXIMP = 0.9999f;
 // fp32 model + env constants, built on the host from pp3_model_t / pp3_env_config_t.
 struct DevModel {
   // ---- per-lane phase records (first: small offsets) ----
-  LaneRec<(LL_WORDS + 3) / 4> lane_lim[32];
-  LaneRec<(LC_WORDS + 3) / 4> lane_com[32];
-  LaneRec<(LM_WORDS + 3) / 4> lane_m[32];
+  LaneTab<(LL_WORDS + 3) / 4> lane_lim;
+  LaneTab<(LC_WORDS + 3) / 4> lane_com;
+  LaneTab<(LM_WORDS + 3) / 4> lane_m;
   // ---- options ----
   float h;
   float gravity[3];
@@ -189,7 +196,7 @@ struct DevModel {
   float key_qpos[NQ];
   float pi_f;
   // last: the same 1 KB inserted after lane_m (shifting every later field) measured 1.3 % slower
-  LaneRec<(LE_WORDS + 3) / 4> lane_env[32];
+  LaneTab<(LE_WORDS + 3) / 4> lane_env;
 };
 
 // ------------------------------- float helpers -------------------------------

@@ -111,13 +111,13 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // together ahead of it and retired by one vmcnt wait, instead of each load being placed (and
 // waited for) right before its first use.
 #define PIN(...) asm volatile("" : __VA_ARGS__)
-// a lane's phase record: N 16-byte loads issued back to back, pinned together
-template <int N>
-__device__ __forceinline__ LaneRec<N> fetch_rec(const LaneRec<N>& src) {
-  const v4f* p = reinterpret_cast<const v4f*>(&src);
+// a record of N 16-byte word groups, group k at p + k * STRIDE floats: N loads issued back to
+// back, pinned together
+template <int N, int STRIDE>
+__device__ __forceinline__ LaneRec<N> fetch_groups(const float* p) {
   v4f v[N];
 #pragma unroll
-  for (int k = 0; k < N; k++) v[k] = p[k];
+  for (int k = 0; k < N; k++) v[k] = *reinterpret_cast<const v4f*>(p + k * STRIDE);
   if constexpr (N == 1) PIN("+v"(v[0]));
   else if constexpr (N == 2) PIN("+v"(v[0]), "+v"(v[1]));
   else if constexpr (N == 3) PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]));
@@ -130,6 +130,16 @@ __device__ __forceinline__ LaneRec<N> fetch_rec(const LaneRec<N>& src) {
 #pragma unroll
     for (int c = 0; c < 4; c++) r.f[4 * k + c] = v[k][c];
   return r;
+}
+// a contiguous record (indexed by pair: PairCon)
+template <int N>
+__device__ __forceinline__ LaneRec<N> fetch_rec(const LaneRec<N>& src) {
+  return fetch_groups<N, 4>(src.f);
+}
+// lane l's phase record from a word-group-major table
+template <int N>
+__device__ __forceinline__ LaneRec<N> fetch_rec(const LaneTab<N>& t, int l) {
+  return fetch_groups<N, 4 * 32>(t.g[0][l]);
 }
 __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 
@@ -276,7 +286,7 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
 // ------------------------------------------------------------------------------------
 template <int NC>
 __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h) {
-  const LaneRec<2> rc = fetch_rec(m.lane_com[l]);
+  const LaneRec<2> rc = fetch_rec(m.lane_com, l);
   const bool body = l >= 1 && l < NB;
   float mb = 0, mx = 0, my = 0, mz = 0;
   if (body) {
@@ -978,7 +988,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   AB_REP(4) { lsup = collision(s, m, l, h); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   {
-    const LaneRec<7> rl = fetch_rec(m.lane_lim[l]);
+    const LaneRec<7> rl = fetch_rec(m.lane_lim, l);
     // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
     bool act = false;
     float value = 0;
@@ -1030,7 +1040,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(2); l = opaque_lane(l);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
-  const LaneRec<3> rm = fetch_rec(m.lane_m[l]);  // (also read by phases 13 and 7)
+  const LaneRec<3> rm = fetch_rec(m.lane_m, l);  // (also read by phases 13 and 7)
   AB_REP(5)
 #pragma unroll
   for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count
@@ -1789,7 +1799,9 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     }
     if (l < NU) act_in = act_env[l];
   }
-  const LaneRec<2> re = m.lane_env[l];
+  LaneRec<2> re;  // plain loads (no pin): retired with the batch's first wait
+  for (int k = 0; k < 2; k++)
+    for (int c = 0; c < 4; c++) re.f[4 * k + c] = m.lane_env.g[k][l][c];
   // observation history: obs_out[36:] = obs_in[:36(H-1)] (environment.py:540-543)
   const int nmove = PP3_OBS_DIM * (m.H - 1);
   float tmp[OBS_MOVE];
@@ -1875,7 +1887,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   asm volatile("" : "+s"(mq));
   {
   const DevModel& m = *(const DevModel*)mq;
-  const LaneRec<2> re = fetch_rec(m.lane_env[l]);  // this lane's env constants (one round trip)
+  const LaneRec<2> re = fetch_rec(m.lane_env, l);  // this lane's env constants (one round trip)
   // ---- observation (history already shifted in the prologue) ----
   get_obs(s, m, gst + m.imu_off, l, h, re.f[LE_POSE16], own, imu_stash);
   {
@@ -2127,7 +2139,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   if (own && l < m.Li) gst[m.imu_off + 5 * m.Li + l] = -1.0f;  // initial_imu_buffer gravity row
   __threadfence_block();
   __syncthreads();  // the gravity row above is global memory written by other lanes
-  get_obs(s, m, gst + m.imu_off, l, h, m.lane_env[l].f[LE_POSE16], own);
+  get_obs(s, m, gst + m.imu_off, l, h, m.lane_env.g[LE_POSE16 / 4][l][LE_POSE16 % 4], own);
   write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, l, own);
   if (own && a.episode) {
     if (l < PP3_EP_STRIDE) a.episode[(size_t)env * PP3_EP_STRIDE + l] = 0.0f;
@@ -2279,9 +2291,15 @@ static void quat2mat_d(const double q[4], double R[9]) {
 
 // the per-lane phase records (pp3_device.h LaneRec) from the already filled model fields
 static void set_i(float& f, int32_t v) { memcpy(&f, &v, 4); }
+template <int N>
+static void put_rec(LaneTab<N>& t, int l, const LaneRec<N>& r) {
+  for (int k = 0; k < N; k++)
+    for (int c = 0; c < 4; c++) t.g[k][l][c] = r.f[4 * k + c];
+}
 static void fill_lane_records(DevModel* d) {
   for (int l = 0; l < 32; l++) {
-    float* f = d->lane_lim[l].f;
+    LaneRec<(LL_WORDS + 3) / 4> rl = {};
+    float* f = rl.f;
     if (l < 2 * (NJ - 1)) {
       const int j = 1 + l / 2, hi = l & 1;
       set_i(f[LL_LIM_ON], d->jnt_limited[j] ? 1 : 0);
@@ -2309,7 +2327,8 @@ static void fill_lane_records(DevModel* d) {
       f[LL_FRANGE] = d->act_frange[l][0];
       f[LL_FRANGE + 1] = d->act_frange[l][1];
     }
-    float* c = d->lane_com[l].f;
+    LaneRec<(LC_WORDS + 3) / 4> rc = {};
+    float* c = rc.f;
     if (l >= 1 && l < NB)
       for (int k = 0; k < 4; k++) c[LC_IQUAT + k] = d->body_iquat[l][k];
     if (l < d->nrobot_geom) {
@@ -2321,7 +2340,8 @@ static void fill_lane_records(DevModel* d) {
       set_i(c[LC_PT_BODY], d->site_body[si]);
       for (int k = 0; k < 3; k++) c[LC_PT_POS + k] = d->site_pos[si][k];
     }
-    float* mr = d->lane_m[l].f;
+    LaneRec<(LM_WORDS + 3) / 4> rm = {};
+    float* mr = rm.f;
     for (int t = 0; t < 4; t++) {
       const int p = l + 32 * t;
       if (p < d->nmpair) {
@@ -2334,7 +2354,8 @@ static void fill_lane_records(DevModel* d) {
     }
     if (l < NV) mr[LM_DAMP] = d->dof_damping[l];
     if (l < NFR) mr[LM_FLOSS] = d->fr_floss[6 + l];
-    float* e = d->lane_env[l].f;
+    LaneRec<(LE_WORDS + 3) / 4> re = {};
+    float* e = re.f;
     if (l < NU) {
       e[LE_POSE] = d->default_pose[l];
       e[LE_JLO] = d->jlo[l];
@@ -2343,6 +2364,10 @@ static void fill_lane_records(DevModel* d) {
     }
     if (l < 4) set_i(e[LE_LEG], d->lower_leg_body[l]);
     if (l >= 16 && l < 16 + NU) e[LE_POSE16] = d->default_pose[l - 16];
+    put_rec(d->lane_lim, l, rl);
+    put_rec(d->lane_com, l, rc);
+    put_rec(d->lane_m, l, rm);
+    put_rec(d->lane_env, l, re);
   }
   for (int p = 0; p < d->npair; p++) {
     const int ga = d->cg_id[d->pair_g1[p]], gb = d->cg_id[d->pair_g2[p]];
