@@ -71,6 +71,10 @@ template <int N>
 struct alignas(16) LaneTab {
   float g[N][32][4];
 };
+// the narrow phase's pair records, laid out the same way (lane = pair within a 32-pair batch)
+struct alignas(16) PairTab {
+  float g[PAIR_REC / 4][PP3_MAX_PAIR][4];
+};
 // phase "limits/friction/actuation": lane l < 24 = joint-limit side (j = 1 + l/2, hi side when
 // l is odd), lane l < 12 = frictionloss row of dof 6+l and actuator l
 enum {
@@ -154,7 +158,7 @@ struct DevModel {
   float pair_tran[PP3_MAX_PAIR];       // body_invweight0 translational sum
   int32_t pair_sup[PP3_MAX_PAIR];      // Jacobian column support: leg 0..3 (+base), 4 base only, 5 dense
   uint32_t pair_dm[PP3_MAX_PAIR][2];   // dof masks (ancestor-or-self) of the pair's two bodies
-  PairRec pair_rec[PP3_MAX_PAIR];      // sphere-box: s2 = -1 - (box slot)
+  PairTab pair_rec;                    // PairRec of pair p, word-group major; sphere-box: s2 = -1 - (box slot)
   PairCon pair_con[PP3_MAX_PAIR];
   float pair_solimp[PP3_MAX_PAIR][5];  // clamped
   // per-env terrain (pp3_set_terrain): TerrainRec[N (padded even)][nbox], or 0 = static boxes

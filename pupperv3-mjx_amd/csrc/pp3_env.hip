@@ -398,10 +398,9 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, i
   // one batch of loads
   PairRec rec;
   {
-    const v4f* src = reinterpret_cast<const v4f*>(&m.pair_rec[p]);
     v4f v[7];
 #pragma unroll
-    for (int k = 0; k < 6; k++) v[k] = src[k];
+    for (int k = 0; k < 6; k++) v[k] = *reinterpret_cast<const v4f*>(m.pair_rec.g[k][p]);
     v[6] = *reinterpret_cast<const v4f*>(&m.pair_con[p]);
     PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]));
     __builtin_memcpy(&rec, v, sizeof(rec));
@@ -2538,7 +2537,7 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
     d->pair_dm[p][0] = d->body_dofmask[mm->cgeom_bodyid[g1]];
     d->pair_dm[p][1] = d->body_dofmask[mm->cgeom_bodyid[g2]];
     {  // flattened narrow-phase record
-      PairRec& r = d->pair_rec[p];
+      PairRec r;
       memset(&r, 0, sizeof(r));
       const int t1 = mm->cgeom_type[g1], t2 = mm->cgeom_type[g2];
       r.kind = (t1 == PP3_GEOM_PLANE && t2 == PP3_GEOM_SPHERE) ? PK_PLANE_SPHERE
@@ -2554,6 +2553,9 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
       for (int k = 0; k < 9; k++) r.R[k] = d->cg_wmat[gf][k];
       if (r.kind == PK_SPHERE_BOX)
         for (int k = 0; k < 3; k++) r.half[k] = d->cg_size[g2][k];
+      const float* rf = reinterpret_cast<const float*>(&r);
+      for (int k = 0; k < PAIR_REC / 4; k++)
+        for (int c = 0; c < 4; c++) d->pair_rec.g[k][p][c] = rf[4 * k + c];
     }
     {  // contact-side record
       PairCon& q = d->pair_con[p];
