@@ -170,3 +170,43 @@ def test_legacy_rng_split_parity(model_path):
         fb.finish()
     finally:
         e.close()
+
+
+def test_collision_reward_terms(env):
+    """Robots dropped onto their knees and torso: rewards.py's knee_collision / body_collision
+    (geom_collision over the contacts with dist < 0; the kernel counts them from per-pair
+    knee/torso counts the host precomputes) against the oracle, plus the other reward terms and
+    obs under many simultaneous contacts (the contact cap's deepest-first ranking included)."""
+    keys = make_keys(3, N)
+    st = env.reset(keys)
+    rs = np.random.RandomState(11)
+    q = st.pipeline_state.q.copy()
+    q[:, 2] = rs.uniform(0.0, 0.05, N)  # torso near the floor: torso and upper legs penetrate
+    for i in range(N):  # small random tilt
+        ax = rs.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        ang = rs.uniform(0, 0.6)
+        q[i, 3:7] = [np.cos(ang / 2), *(np.sin(ang / 2) * ax)]
+    st.pipeline_state.q = q
+    rec = st._record.copy()
+    rec[:, _abi.S_QPOS:_abi.S_QPOS + 19] = q
+    a = np.zeros((N, 12), np.float32)
+    out = env.step(st, a)
+    oe = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f32")
+    ik = 1 + _abi.REWARD_NAMES.index("knee_collision")
+    ib = 1 + _abi.REWARD_NAMES.index("body_collision")
+    fb = G.FlipBudget(max_frac=0.1)
+    hits_k = hits_b = 0
+    for i in range(N):
+        o = oe.step(dict(state=G.record_to_oracle_state(rec[i]), obs=st.obs[i].astype(np.float64)),
+                    a[i].astype(np.float64))
+        gk, gb = out.metrics["knee_collision"][i], out.metrics["body_collision"][i]
+        hits_k += o["metrics"][ik] != 0
+        hits_b += o["metrics"][ib] != 0
+        ok = (gk == np.float32(o["metrics"][ik]) and gb == np.float32(o["metrics"][ib])
+              and abs(out.reward[i] - o["reward"]) <= 1e-3 and out.done[i] == o["done"])
+        fb.check(ok, o, f"env {i}: knee {gk} vs {o['metrics'][ik]}, body {gb} vs {o['metrics'][ib]}")
+    fb.finish()
+    # the knee term is exercised; body_collision stays 0 on both sides here: the test model's
+    # only torso geom is a visual mesh (contype 0), so no torso pair exists
+    assert hits_k >= N // 4 and hits_b == 0, (hits_k, hits_b)
