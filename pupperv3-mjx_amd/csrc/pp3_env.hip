@@ -285,8 +285,7 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
 // lanes 1..13 bodies, 14..31 dofs; then lanes 0..7 geoms, 16..19 feet.
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h) {
-  const LaneRec<2> rc = fetch_rec(m.lane_com, l);
+__device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h, const LaneRec<2>& rc) {
   const bool body = l >= 1 && l < NB;
   float mb = 0, mx = 0, my = 0, mz = 0;
   if (body) {
@@ -976,9 +975,26 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #define PP3_AB_DUP 0
 #endif
 #define AB_REP(k) for (int ab_r_ = 0; ab_r_ < (PP3_AB_DUP == (k) ? 2 : 1); ab_r_++)
+  // the com and M-entry phases' lane records, loaded here without a wait: they arrive while
+  // kinematics runs (a pinned fetch at the phase itself costs a round trip there)
+  LaneRec<2> rc_pf;
+  LaneRec<3> rm_pf;
+  {
+    v4f v[5];
+#pragma unroll
+    for (int k = 0; k < 2; k++) v[k] = *reinterpret_cast<const v4f*>(m.lane_com.g[k][l]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) v[2 + k] = *reinterpret_cast<const v4f*>(m.lane_m.g[k][l]);
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+      for (int c = 0; c < 4; c++) rc_pf.f[4 * k + c] = v[k][c];
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      for (int c = 0; c < 4; c++) rm_pf.f[4 * k + c] = v[2 + k][c];
+  }
   AB_REP(1) { kinematics(s, m, l); SYNC(); }
   PHASE(0); l = opaque_lane(l);
-  AB_REP(2) { com_pos(s, m, l, h); SYNC(); }
+  AB_REP(2) { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
   AB_REP(3) { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
@@ -1039,7 +1055,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(2); l = opaque_lane(l);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
-  const LaneRec<3> rm = fetch_rec(m.lane_m, l);  // (also read by phases 13 and 7)
+  const LaneRec<3> rm = rm_pf;  // (prefetched at the substep start; also read by phases 13 and 7)
   AB_REP(5)
 #pragma unroll
   for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count
