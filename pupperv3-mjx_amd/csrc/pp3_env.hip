@@ -1002,6 +1002,16 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   int lsup = 4;  // lane c: support of contact c (4 = none)
   AB_REP(4) { lsup = collision(s, m, l, h); SYNC(); }
   PHASE(16); l = opaque_lane(l);
+  // the PairCon of contact c = l / 4 for the first batch of phase 13's edge rows (lane e = 4c + k),
+  // loaded here unpinned: it arrives during the limit/actuation and M-entry phases
+  v4f pcv[4];
+  {
+    const int c = l >> 2;
+    const int p = c < s.ncon ? s.con_pair[c < NC ? c : 0] : 0;
+    const v4f* src = reinterpret_cast<const v4f*>(&m.pair_con[p]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) pcv[k] = src[k];
+  }
   {
     const LaneRec<7> rl = fetch_rec(m.lane_lim, l);
     // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
@@ -1115,7 +1125,15 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   const int nefc = NFR + nl + 4 * ncon;
   for (int e = l; e < 4 * ncon; e += HW) {
     const int c = e >> 2, p = s.con_pair[c], r = NFR + nl + e;
-    const LaneRec<4> pc = fetch_rec(*reinterpret_cast<const LaneRec<4>*>(&m.pair_con[p]));
+    LaneRec<4> pc;
+    if (e < HW) {  // first batch (every row when 4 * ncon <= 32): prefetched after the collision
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) pc.f[4 * k + cc] = pcv[k][cc];
+    } else {
+      pc = fetch_rec(*reinterpret_cast<const LaneRec<4>*>(&m.pair_con[p]));
+    }
     const PairCon& q = *reinterpret_cast<const PairCon*>(&pc);
     const float mu = s.con_mu[c];
     const float dist = s.con_dist[c];
