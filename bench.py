@@ -10,6 +10,10 @@ HBM (synthetic).  Multi-GPU: one process per GPU (torch.distributed.run), envs s
 data-path collective (weak scaling); barrier + max-over-ranks timing over RCCL.
 
   python bench.py [--gpus N --steps K --warmup W --envs E --dr --gather --no-cpu-baseline]
+
+No torch: multi-GPU ranks (RANK / WORLD_SIZE / LOCAL_RANK from torch.distributed.run or any
+launcher) talk through the library's own RCCL communicator (pp3_comm_*: barrier, max-over-ranks
+timing, the --gather collective), created from an id exchanged by a file rendezvous on the node.
 """
 import argparse
 import ctypes as C
@@ -24,7 +28,13 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "pupperv3-mjx_amd")]
 METRIC = "env-steps/sec at N_envs=4096/GPU, 1/2/4/8 MI355X; qpos rel-err vs mj_step"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFLOPS = 157.3    # vector FP32 (spec)
-N_SIMD, CLOCK_HZ, VALU_CYC = 1024, 2.4e9, 4   # 256 CUs x 4 SIMDs; peak engine clock; wave64 VALU issue
+# 256 CUs x 4 SIMDs; peak engine clock; a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+# when the SIMD is fed by >= 2 waves (MI355X_MICROARCH.md "Wave scheduling"; one wave alone
+# sustains one per 4 cycles).  Transcendentals are counted at the plain rate (a lower bound).
+N_SIMD, CLOCK_HZ, VALU_CYC = 1024, 2.4e9, 2
+KERNEL_SOURCES = ("pupperv3-mjx_amd/csrc/pp3_env.hip", "pupperv3-mjx_amd/csrc/pp3_device.h",
+                  "pupperv3-mjx_amd/csrc/Makefile")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_current.json")
 
 
 def algorithmic_bytes_per_env_step(stride: int, H: int, dr: bool) -> int:
@@ -48,6 +58,88 @@ def bench_kwargs(model_path, random_commands=False):
             x_min=-1.0, x_max=1.0, y_min=-1.0, y_max=1.0, z_min=0.18, z_max=0.24),
         kick_vel=1.0, kick_probability=0.04, terminal_body_z=0.1, early_termination_step_threshold=500,
     )
+
+
+def kernel_source_sha16() -> str:
+    """Hash of the sources the step kernel is built from: a PMC profile (profiles/traffic_current.json)
+    is only used for the kernel it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        h.update(open(os.path.join(ROOT, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def _oracle_record(rec):
+    """Device f32 state record (RNG words bit-cast) -> the oracle's float64 record."""
+    import numpy as np
+    from pupperv3_mjx import _abi
+    with np.errstate(invalid="ignore"):
+        out = rec.astype(np.float64)
+    out[..., _abi.S_RNG:_abi.S_RNG + 2] = rec[..., _abi.S_RNG:_abi.S_RNG + 2].copy().view(np.uint32)
+    return out
+
+
+def one_step_err(env, n_sample=256, seed=0):
+    """SURVEY 7 hard part 2: one env step (n_frames substeps) of the fp32 kernel vs the fp64 oracle
+    restatement from IDENTICAL states, on the workload's own states after the timed run."""
+    import numpy as np
+    from pupperv3_mjx import _abi, _lib
+    from oracle import oracle as O
+    E = env.num_envs
+    rec0 = env._get(_abi.F_STATE)
+    obs0 = env._get(_abi.F_OBS)
+    a = np.random.RandomState(seed).uniform(-1, 1, size=(E, 12)).astype(np.float32)
+    buf = _lib.DeviceBuffer(a.nbytes, env.device)
+    buf.upload(a)
+    env.step_device(buf.ptr.value)
+    env.synchronize()
+    rec1 = env._get(_abi.F_STATE)
+    buf.free()
+    ids = np.random.RandomState(seed + 1).choice(E, size=min(n_sample, E), replace=False)
+    oe = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f64")
+    dq, dv, rq, flagged = [], [], [], []
+    for i in ids:
+        o = oe.step(dict(state=_oracle_record(rec0[i]), obs=obs0[i].astype(np.float64)), a[i].astype(np.float64))
+        q_o, v_o = o["state"][0:19], o["state"][19:37]
+        dq.append(np.abs(rec1[i, 0:19] - q_o).max())
+        dv.append(np.abs(rec1[i, 19:37] - v_o).max())
+        rq.append(np.abs(rec1[i, 0:19] - q_o).max() / max(np.abs(q_o).max(), 1e-9))
+        flagged.append(o["boundary"] > 0)
+    dq, dv, rq, flagged = map(np.array, (dq, dv, rq, flagged))
+
+    def st(x):
+        return {"max": float(x.max()), "median": float(np.median(x)), "p99": float(np.percentile(x, 99))}
+
+    ok = ~flagged
+    return {"envs": int(len(ids)), "substeps": int(env._n_frames), "vs": "fp64 oracle restatement, identical start state",
+            "qpos_abs": st(dq), "qvel_abs": st(dv), "qpos_rel": st(rq),
+            "constraint_flip_envs": int(flagged.sum()),
+            "qpos_abs_max_unflagged": float(dq[ok].max()) if ok.any() else None,
+            "qvel_abs_max_unflagged": float(dv[ok].max()) if ok.any() else None}
+
+
+def contact_cap_stats(env, acts_ptr, steps):
+    """Untimed: `steps` env steps with the pipeline record on; counts env steps whose penetrating
+    pairs exceed the contact cap (PP3_P_NHIT > the kernel's cap): where the cap binds, the kernel
+    (like the oracle) keeps the deepest and departs from MuJoCo-CPU's keep-all."""
+    import numpy as np
+    from pupperv3_mjx import _abi, _lib
+    cap = env.config_struct.ncon_max or 8
+    _lib.check(env._L.pp3_set_pipeline_output(env._h, 1))
+    over = 0
+    max_hit = 0
+    hist = None
+    for i in range(steps):
+        env.step_device(acts_ptr + i * env.num_envs * 48)
+        p = env._get(_abi.F_PIPELINE)
+        nhit = p[:, _abi.P_NHIT].astype(int)
+        over += int((nhit > cap).sum())
+        max_hit = max(max_hit, int(nhit.max()))
+        hist = np.bincount(p[:, _abi.P_NCON].astype(int), minlength=cap + 1).tolist()
+    _lib.check(env._L.pp3_set_pipeline_output(env._h, 0))
+    return {"cap": int(cap), "env_steps": int(steps * env.num_envs), "overflow_env_steps": over,
+            "max_penetrating_pairs": max_hit, "active_contact_hist_last_step": hist}
 
 
 def cpu_baseline(model, cfg, states, obs, seconds_target=12.0):
@@ -112,7 +204,9 @@ def main():
                     help="per-env terrain (SURVEY 8f rank 3): every env gets its own random boxes in the --obstacles slots")
     ap.add_argument("--random-commands", action="store_true",
                     help="keep the reset's sampled velocity commands (configs[3]) instead of the fixed (0.5,0,0)")
-    ap.add_argument("--gather", action="store_true", help="RCCL all_gather of obs|reward|done per step (configs[3])")
+    ap.add_argument("--gather", action="store_true",
+                    help="per-step RCCL hand-over of obs|reward|done to the learner rank (configs[3])")
+    ap.add_argument("--gather-root", type=int, default=0, help="learner rank of --gather; -1 = all-gather")
     ap.add_argument("--auto-reset", type=int, default=0, metavar="EPISODE_LENGTH",
                     help="on-device EpisodeWrapper+AutoResetWrapper (brax training wrap) with this episode length")
     ap.add_argument("--policy", type=str, default="", metavar="H1,H2,...",
@@ -121,30 +215,22 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency-floor", action="store_true",
                     help="skip the E/2-envs latency-floor launches (keeps rocprof stats to E-env launches)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the untimed accuracy / contact-cap measurements (profiling runs)")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal knobs for the multi-rank path on a single GPU (never used by the driver):
-    # PP3_BENCH_DEVICE pins every rank to one device, PP3_BENCH_BACKEND=gloo avoids RCCL's
-    # one-rank-per-GPU rule
+    # rehearsal knob for the multi-rank code on one GPU (never used by the driver): every rank on
+    # this device
     device = int(os.environ.get("PP3_BENCH_DEVICE", local_rank))
-    backend = os.environ.get("PP3_BENCH_BACKEND", "nccl")
-    # torch first: its bundled libamdhip64.so.7 then also serves libpupper_hip.so (one HIP runtime)
-    import torch
-    import torch.distributed as dist
     import numpy as np
-    torch.cuda.set_device(device)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group(backend, rank=rank, world_size=world)
-
     from pupperv3_mjx import MODEL_XML, _abi, _lib, sharding
     from pupperv3_mjx.environment import PupperV3Env
+
+    comm = sharding.Comm(rank, world, device) if world > 1 else None
 
     model_path = MODEL_XML
     if args.obstacles:
@@ -184,18 +270,22 @@ def main():
     acts = _lib.DeviceBuffer(total * E * 12 * 4, device)
     _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, total * E * 12, 1234 + rank, 0, -1.0, 1.0, None))
     env.synchronize()
+    act_at = lambda i: acts.ptr.value + i * E * 48  # noqa: E731  (actions of step i)
     ms = C.c_float()
     if args.warmup:
         _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, args.warmup, C.byref(ms)))
-    gather_buf = None
-    if args.gather and world > 1:
-        obs_n = env.device_field(_abi.F_OBS)[1]
-        gather_buf = (torch.empty((E, obs_n), device="cuda"), torch.empty(E, device="cuda"),
-                      torch.empty(E, device="cuda"))
+    gather_dst, nmax = None, 0
+    if args.gather:
+        nmax = E  # equal shards: every rank contributes E rows of width 36H + 2
+        width = env.observation_size + 2
+        if args.gather_root < 0 or rank == args.gather_root:
+            gather_dst = _lib.DeviceBuffer(world * nmax * width * 4, device)
+        if comm is None:  # one rank: the gather is a pack (a one-rank communicator still runs it)
+            comm = sharding.Comm(0, 1, device, tag="_solo")
 
     def barrier():
-        if world > 1:
-            dist.barrier()
+        if comm is not None and comm.world > 1:
+            comm.barrier()
 
     policy = None
     if args.policy:
@@ -214,9 +304,8 @@ def main():
             policy.act_env(env, acts.ptr.value)
             env.step_device(acts.ptr.value)
 
-    barrier()
-    torch.cuda.synchronize()
     env.synchronize()
+    barrier()
     t0 = time.perf_counter()
     if policy is not None:
         for i in range(args.steps):
@@ -224,41 +313,43 @@ def main():
             env.step_device(acts.ptr.value)
         env.synchronize()
         kernel_ms = (time.perf_counter() - t0) * 1e3  # policy + env step per iteration (no per-kernel events)
-    elif gather_buf is None:
-        _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + args.warmup * E * 12 * 4), E * 12,
-                                    args.steps, C.byref(ms)))
+    elif not args.gather:
+        _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps, C.byref(ms)))
         kernel_ms = ms.value
     else:
-        kernel_ms = 0.0
-        obs_t, rew_t, done_t = gather_buf
+        # step kernel, then the RCCL hand-over of its outputs, both on the env's stream: no host sync
         for i in range(args.steps):
-            _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + (args.warmup + i) * E * 48), 0, 1,
-                                        C.byref(ms)))
-            kernel_ms += ms.value
-            env.synchronize()  # step ran on the handle's stream; copies + gather go on torch's (null) stream
-            for fid, t in ((_abi.F_OBS, obs_t), (_abi.F_REWARD, rew_t), (_abi.F_DONE, done_t)):
-                ptr, _ = env.device_field(fid)
-                _lib.check(L.pp3_memcpy_d2d(C.c_void_p(t.data_ptr()), C.c_void_p(ptr), t.numel() * 4, None))
-            sharding.gather_batch(obs_t, rew_t, done_t, E * world)
+            env.step_device(act_at(args.warmup + i))
+            comm.gather(env, nmax, gather_dst.ptr.value if gather_dst else None, root=args.gather_root)
+        kernel_ms = None
     env.synchronize()
-    torch.cuda.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max, kernel_ms_max = float(t[0]), float(t[1])
+    gather_info = None
+    if args.gather:
+        # untimed: the same K steps' kernels alone (events), then the gather alone
+        _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps, C.byref(ms)))
+        kernel_ms = ms.value
+        env.synchronize()
+        barrier()
+        tg = time.perf_counter()
+        for i in range(args.steps):
+            comm.gather(env, nmax, gather_dst.ptr.value if gather_dst else None, root=args.gather_root)
+        env.synchronize()
+        barrier()
+        gather_s = (time.perf_counter() - tg) / args.steps
+        gather_info = {"root": args.gather_root, "rows_per_rank": nmax, "row_floats": env.observation_size + 2,
+                       "bytes_per_rank": nmax * (env.observation_size + 2) * 4,
+                       "ms_per_gather": round(gather_s * 1e3, 4), "transport": "RCCL (pp3_gather), env stream"}
+    if comm is not None and comm.world > 1:
+        wall_max, kernel_ms_max = (float(v) for v in comm.allreduce([wall, kernel_ms], "max"))
+    else:
+        wall_max, kernel_ms_max = wall, kernel_ms
 
     # sanity on the produced batch
     rew = env._get(_abi.F_REWARD)
     obs = env._get(_abi.F_OBS)
     assert np.all(np.isfinite(rew)) and np.all(np.isfinite(obs)), "non-finite env outputs"
-    # active-contact histogram of one further (untimed) step, from the Brax-pipeline record
-    _lib.check(L.pp3_set_pipeline_output(env._h, 1))
-    env.step_device(acts.ptr.value)
-    env.synchronize()
-    ncon = env._get(_abi.F_PIPELINE)[:, _abi.P_NCON].astype(int)
-    contact_hist = np.bincount(ncon, minlength=9).tolist()
 
     if rank == 0:
         K = args.steps
@@ -266,14 +357,15 @@ def main():
         launch_s = kernel_ms_max / 1e3 / K
         bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr)
         achieved = bpe * E / launch_s / 1e9
-        traffic, valu, epw = None, None, 1
-        tpath = os.path.join(ROOT, "profiles", "traffic_r01.json")
-        if os.path.exists(tpath):
-            tj = json.load(open(tpath))
-            if tj.get("envs") == E and tj.get("dr", False) == args.dr and not args.obstacles:
+        traffic, valu, epw, tsrc = None, None, 2, None
+        if os.path.exists(TRAFFIC_FILE):
+            tj = json.load(open(TRAFFIC_FILE))
+            if (tj.get("src_sha16") == kernel_source_sha16() and tj.get("envs") == E
+                    and tj.get("dr", False) == args.dr and not args.obstacles):
                 traffic = tj.get("hbm_bytes_per_launch")
                 valu = tj.get("valu_insts_per_wave")
-                epw = tj.get("envs_per_wave", 1)
+                epw = tj.get("envs_per_wave", 2)
+                tsrc = tj.get("source")
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -292,27 +384,29 @@ def main():
                                        "random commands" if args.random_commands else "fixed command (0.5,0,0)",
                                        "domain randomisation" if args.dr else "no DR")),
                        "envs_per_gpu": E, "global_envs": E * world, "obs_history": env._observation_history,
-                       "n_frames": env._n_frames, "parallelism": f"env-sharded x{world} (no data-path collective)",
+                       "n_frames": env._n_frames, "parallelism": f"env-sharded x{world} (no data-path collective)"
+                       if not args.gather else f"env-sharded x{world} + per-step RCCL gather to rank {args.gather_root}",
                        "per_env_terrain": bool(args.terrain),
                        "commands": "reset-sampled, resampled every 500 steps" if args.random_commands else "fixed (0.5,0,0)",
-                       "gather": bool(gather_buf is not None), "auto_reset_episode_length": args.auto_reset or None,
+                       "gather": gather_info, "auto_reset_episode_length": args.auto_reset or None,
                        "policy_in_loop": args.policy or None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": "pp3::env_step_kernel", "bytes_per_env_step": bpe,
-                         "avg_launch_ms": round(launch_s * 1e3, 4)},
-            "active_contacts": {"hist": contact_hist, "mean": round(float(np.mean(ncon)), 3),
-                                "note": "contacts per env after the run (rank 0's shard)"},
+                         "avg_launch_ms": round(launch_s * 1e3, 4),
+                         "traffic_source": tsrc or "none for this kernel build (profiles/traffic_current.json "
+                                                   "src_sha16 != the kernel sources' hash)"},
         }
         if valu:
-            # Compute-side bound (DESIGN.md 'Roofline'): VALU issue.  One wave = `epw` envs; a wave64
-            # VALU instruction occupies its SIMD for 4 cycles; 1024 SIMDs at 2.4 GHz.
+            # Compute-side bound: VALU issue.  One wave = `epw` envs; E/epw waves over
+            # 1024 SIMDs; a wave64 VALU instruction holds its SIMD for VALU_CYC cycles at 2.4 GHz.
             ceil_s = valu * VALU_CYC * (E / epw) / (N_SIMD * CLOCK_HZ)
             out["roofline"]["valu_issue"] = {"valu_insts_per_wave": valu, "envs_per_wave": epw,
+                                             "cycles_per_valu": VALU_CYC,
                                              "ceiling_ms": round(ceil_s * 1e3, 4),
                                              "frac": round(ceil_s / launch_s, 4),
-                                             "source": "profiles/traffic_r01.json (rocprofv3 SQ_INSTS_VALU)"}
-        if (world == 1 and policy is None and gather_buf is None and E == 4096 and not args.dr and not args.obstacles
+                                             "source": "profiles/traffic_current.json (rocprofv3 SQ_INSTS_VALU)"}
+        if (world == 1 and policy is None and not args.gather and E == 4096 and not args.dr and not args.obstacles
                 and not args.auto_reset and not args.no_latency_floor):
             # Latency floor: the same step at E/2 envs puts ONE wave (two envs)
             # on each SIMD; the kernel then takes one wave's critical path.  ratio = launch time at E
@@ -332,20 +426,22 @@ def main():
                                           "avg_launch_ms": round(half_s * 1e3, 4),
                                           "ratio": round(launch_s / half_s, 4),
                                           "note": "launch time at E / at E/2 envs (one wave per SIMD)"}
-        if world == 1:
+        if world == 1 and not args.no_extras:
+            out["contact_cap"] = contact_cap_stats(env, acts.ptr.value, min(K, 50))
+            out["one_step_err"] = one_step_err(env)
             out["qpos_rel_err"] = {"value": qpos_drift(env), "substeps": 1000,
                                    "vs": "fp64 oracle restatement (MuJoCo absent; parity unpinned vs mj_step)",
                                    "trajectory": "standing PD hold"}
             if not args.no_cpu_baseline:
-                with np.errstate(invalid="ignore"):  # RNG words are bit-cast uint32 in the f32 record
-                    states = rec.astype(np.float64)
-                states[:, _abi.S_RNG:_abi.S_RNG + 2] = rec[:, _abi.S_RNG:_abi.S_RNG + 2].copy().view(np.uint32)
+                states = _oracle_record(rec)
                 out["cpu_baseline"] = cpu_baseline(env.sys_model.struct, env.config_struct, states,
                                                    init_obs.astype(np.float64))
         print(json.dumps(out), flush=True)
+    if gather_dst is not None:
+        gather_dst.free()
     env.close()
-    if world > 1:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.close()
 
 
 if __name__ == "__main__":

@@ -261,7 +261,11 @@ enum {
   PP3_S_ACT_BUF = 98       /* 12*La action buffer [12][La], then 6*Li imu buffer [6][Li] */
 };
 
-/* Field ids for pp3_field / pp3_copy_field. */
+/* Field ids for pp3_field / pp3_copy_field.  Every field is ONE device buffer owned by the
+ * handle, allocated at pp3_create and updated in place: the pointer pp3_field returns stays
+ * valid (and constant) until pp3_destroy, so a training loop may wrap it once; its contents are
+ * overwritten by every pp3_step / pp3_reset launched on the handle's stream (copy a field out
+ * first, on that stream, to keep a previous step's values). */
 enum {
   PP3_F_STATE = 0,    /* [N][state_stride] f32 */
   PP3_F_OBS = 1,      /* [N][36H] f32 */
@@ -290,6 +294,7 @@ enum {
   PP3_P_CON_DIST = 218,     /* 16  dist of contacts 0..15                  */
   PP3_P_CON_GEOM = 234,     /* 32  geom1, geom2 of contacts 0..15 (float)  */
   PP3_P_SUBTREE_COM = 266,  /*  3 */
+  PP3_P_NHIT = 269,         /*  1  penetrating pairs before the contact cap (> ncon: the cap bound) */
   PP3_P_SENSOR = 272,       /* 32  mjData.sensordata (model's <sensor>) */
   PP3_PIPE_STRIDE = 304
 };
@@ -310,7 +315,8 @@ enum {
   PP3_ERR_ARG = 1,
   PP3_ERR_MODEL = 2,   /* model topology / options unsupported          */
   PP3_ERR_HIP = 3,
-  PP3_ERR_NOMEM = 4
+  PP3_ERR_NOMEM = 4,
+  PP3_ERR_COMM = 5     /* RCCL unavailable or a collective failed        */
 };
 
 int pp3_abi_version(void);
@@ -423,6 +429,36 @@ int pp3_policy_act(pp3_policy_t* policy, const float* obs_dev, int64_t obs_strid
 int pp3_policy_out_dim(const pp3_policy_t* policy);
 int pp3_policy_destroy(pp3_policy_t* policy);
 const char* pp3_policy_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Multi-GPU (no reference code: the reference runs one process per device under
+ * Brax PPO's pmap, [ext] brax 0.12.1 brax/training/agents/ppo/train.py, where the env batch is
+ * sharded across devices and XLA gathers it).  One process per GPU, each owning a contiguous
+ * shard of the global env batch (pupperv3_mjx/sharding.py); envs never exchange data inside a
+ * step.  The only data-path collective is the optional per-step hand-over of the learner batch
+ * obs | reward | done over RCCL (xGMI), launched on the env's stream behind the step kernel with
+ * no host synchronisation.  RCCL is dlopen'ed on first use (the single-GPU path never loads it).
+ * ------------------------------------------------------------------------------------- */
+typedef struct pp3_comm pp3_comm_t;
+#define PP3_COMM_ID_BYTES 128 /* ncclUniqueId */
+enum { PP3_REDUCE_SUM = 0, PP3_REDUCE_MAX = 1 };
+/* Rank 0 creates the communicator id and hands its 128 bytes to the other ranks out of band. */
+int pp3_comm_unique_id(uint8_t* id_out);
+int pp3_comm_init(const uint8_t* id, int32_t rank, int32_t world, int32_t device, pp3_comm_t** out);
+int pp3_comm_destroy(pp3_comm_t* comm);
+int32_t pp3_comm_rank(const pp3_comm_t* comm);
+int32_t pp3_comm_world(const pp3_comm_t* comm);
+const char* pp3_comm_last_error(void);
+/* Learner batch of every rank's env shard: each rank contributes nmax rows (nmax >= its env
+ * count; rows past the count are zero) of width 36H + 2 = [obs | reward | done], rank r's rows
+ * at dst_dev + r * nmax * (36H + 2).  root >= 0: gather to rank `root` (grouped send/recv,
+ * dst_dev needed on the root only); root < 0: all-gather (dst_dev on every rank).  Enqueued on
+ * `stream` (NULL = the env's stream): ordered after the env's last step, no host sync. */
+int pp3_gather(pp3_comm_t* comm, pp3_env_t* env, int32_t nmax, int32_t root, float* dst_dev, void* stream);
+/* Host-blocking helpers for timing: element-wise sum / max of n <= 64 doubles over ranks, and
+ * a barrier. */
+int pp3_comm_allreduce(pp3_comm_t* comm, const double* in, double* out, int32_t n, int32_t op);
+int pp3_comm_barrier(pp3_comm_t* comm);
 
 #ifdef __cplusplus
 }

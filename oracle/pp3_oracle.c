@@ -1260,6 +1260,7 @@ static void write_pipeline(const Model* m, const Data* d, real* p) {
   }
   for (int i = 0; i < NV; i++) { p[PP3_P_QFRC_ACT + i] = d->qfrc_actuator[i]; p[PP3_P_QACC + i] = d->qacc[i]; }
   p[PP3_P_NCON] = (real)d->ncon;
+  p[PP3_P_NHIT] = (real)d->ncon_all;
   for (int c = 0; c < d->ncon && c < 16; c++) {
     p[PP3_P_CON_DIST + c] = d->con[c].dist;
     p[PP3_P_CON_GEOM + 2 * c] = (real)m->cg_id[d->con[c].g1];

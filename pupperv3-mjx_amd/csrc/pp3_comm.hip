@@ -1,0 +1,245 @@
+// pp3_comm.hip -- multi-GPU env shards: the one collective of the hot path.
+//
+// Envs are independent, so every GPU steps its own contiguous shard with no exchange inside
+// the step.  The only data-path collective is the optional per-step hand-over of the
+// learner batch obs | reward | done (BASELINE.json north_star: "a single RCCL gather over
+// xGMI for the returned batch"):
+//
+//   pack_kernel   the shard's rows [nmax][D + 2] (obs, reward, done; rows past the shard's
+//                 env count zero-padded so every rank contributes the same count), read from
+//                 the env's device fields on the env's stream -- no host synchronisation;
+//   gather        root >= 0: grouped ncclSend / ncclRecv to the learner rank (each peer's
+//                 chunk crosses its own xGMI link to the root once -- a point-to-point mesh,
+//                 so no ring relay); root < 0: ncclAllGather (every rank gets the batch).
+//
+// RCCL is loaded lazily with dlopen (librccl.so.1 from /opt/rocm/lib), so the single-GPU path
+// never maps it.  The unique id is created by rank 0 (pp3_comm_unique_id) and handed to the
+// other ranks out of band (pupperv3_mjx/sharding.py: a file rendezvous on the node).  No torch.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <string>
+
+#include "pupper_hip.h"
+
+namespace {
+
+struct Rccl {
+  void* so = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+thread_local std::string g_cerr;
+int cerr(int code, const std::string& m) {
+  g_cerr = m;
+  return code;
+}
+
+const Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (tried) return r.so ? &r : nullptr;
+  tried = true;
+  const char* names[] = {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
+  for (const char* n : names)
+    if ((r.so = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+  if (!r.so) {
+    g_cerr = std::string("cannot load librccl.so.1: ") + dlerror();
+    return nullptr;
+  }
+#define SYM(field, name)                                                          \
+  r.field = reinterpret_cast<decltype(r.field)>(dlsym(r.so, name));               \
+  if (!r.field) {                                                                 \
+    g_cerr = std::string("librccl.so.1 lacks ") + name;                           \
+    r.so = nullptr;                                                               \
+    return nullptr;                                                               \
+  }
+  SYM(GetUniqueId, "ncclGetUniqueId")
+  SYM(CommInitRank, "ncclCommInitRank")
+  SYM(CommDestroy, "ncclCommDestroy")
+  SYM(AllGather, "ncclAllGather")
+  SYM(AllReduce, "ncclAllReduce")
+  SYM(Send, "ncclSend")
+  SYM(Recv, "ncclRecv")
+  SYM(GroupStart, "ncclGroupStart")
+  SYM(GroupEnd, "ncclGroupEnd")
+  SYM(GetErrorString, "ncclGetErrorString")
+#undef SYM
+  return &r;
+}
+
+#define HCHK(x)                                                                                   \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) return cerr(PP3_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define NCHK(R, x)                                                                                  \
+  do {                                                                                              \
+    ncclResult_t r_ = (x);                                                                          \
+    if (r_ != ncclSuccess) return cerr(PP3_ERR_COMM, std::string(#x) + ": " + (R)->GetErrorString(r_)); \
+  } while (0)
+
+// learner rows of one shard: out[row][0:D] = obs, [D] = reward, [D+1] = done; rows >= n zero.
+// One thread per output float (coalesced in both the obs reads and the packed writes).
+__global__ void pack_kernel(const float* __restrict__ obs, const float* __restrict__ rew,
+                            const float* __restrict__ done, int n, int D, int nmax, float* __restrict__ out) {
+  const int W = D + 2;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)nmax * W) return;
+  const int row = (int)(i / W), c = (int)(i - (long)row * W);
+  float v = 0.0f;
+  if (row < n) v = c < D ? obs[(long)row * D + c] : (c == D ? rew[row] : done[row]);
+  out[i] = v;
+}
+
+}  // namespace
+
+struct pp3_comm {
+  int rank, world, device;
+  ncclComm_t comm;
+  hipStream_t stream;  // host-blocking helpers (barrier, reductions)
+  float* pack;         // [nmax][D+2] staging of this rank's chunk (allgather / non-root)
+  size_t pack_elems;
+  double* red;         // reduction scratch
+};
+
+extern "C" {
+
+const char* pp3_comm_last_error(void) { return g_cerr.c_str(); }
+
+int pp3_comm_unique_id(uint8_t* out) {
+  if (!out) return cerr(PP3_ERR_ARG, "pp3_comm_unique_id: null output");
+  const Rccl* R = rccl();
+  if (!R) return cerr(PP3_ERR_COMM, g_cerr);
+  ncclUniqueId id;
+  NCHK(R, R->GetUniqueId(&id));
+  static_assert(sizeof(id) == PP3_COMM_ID_BYTES, "ncclUniqueId size");
+  memcpy(out, &id, sizeof(id));
+  return PP3_OK;
+}
+
+int pp3_comm_init(const uint8_t* id, int32_t rank, int32_t world, int32_t device, pp3_comm_t** out) {
+  if (!id || !out || world < 1 || rank < 0 || rank >= world) return cerr(PP3_ERR_ARG, "pp3_comm_init: bad argument");
+  const Rccl* R = rccl();
+  if (!R) return cerr(PP3_ERR_COMM, g_cerr);
+  HCHK(hipSetDevice(device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  pp3_comm* c = new pp3_comm();
+  memset(c, 0, sizeof(*c));
+  c->rank = rank;
+  c->world = world;
+  c->device = device;
+  ncclResult_t r = R->CommInitRank(&c->comm, world, uid, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return cerr(PP3_ERR_COMM, std::string("ncclCommInitRank: ") + R->GetErrorString(r));
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->red, 64 * sizeof(double)) != hipSuccess) {
+    R->CommDestroy(c->comm);
+    delete c;
+    return cerr(PP3_ERR_HIP, "pp3_comm_init: stream / scratch allocation failed");
+  }
+  *out = c;
+  return PP3_OK;
+}
+
+int pp3_comm_destroy(pp3_comm_t* c) {
+  if (!c) return PP3_OK;
+  const Rccl* R = rccl();
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (R) R->CommDestroy(c->comm);
+  (void)hipFree(c->pack);
+  (void)hipFree(c->red);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return PP3_OK;
+}
+
+int32_t pp3_comm_rank(const pp3_comm_t* c) { return c ? c->rank : -1; }
+int32_t pp3_comm_world(const pp3_comm_t* c) { return c ? c->world : 0; }
+
+int pp3_gather(pp3_comm_t* c, pp3_env_t* e, int32_t nmax, int32_t root, float* dst_dev, void* stream) {
+  if (!c || !e) return cerr(PP3_ERR_ARG, "pp3_gather: null argument");
+  if (root >= c->world) return cerr(PP3_ERR_ARG, "pp3_gather: root out of range");
+  const int n = pp3_num_envs(e);
+  if (nmax < n) return cerr(PP3_ERR_ARG, "pp3_gather: nmax smaller than this rank's shard");
+  if ((root < 0 || root == c->rank) && !dst_dev) return cerr(PP3_ERR_ARG, "pp3_gather: null destination");
+  const Rccl* R = rccl();
+  if (!R) return cerr(PP3_ERR_COMM, g_cerr);
+  void *obs, *rew, *done;
+  int64_t D, one;
+  if (pp3_field(e, PP3_F_OBS, &obs, &D) || pp3_field(e, PP3_F_REWARD, &rew, &one) ||
+      pp3_field(e, PP3_F_DONE, &done, &one))
+    return cerr(PP3_ERR_ARG, std::string("pp3_gather: ") + pp3_last_error());
+  const size_t W = (size_t)D + 2, count = (size_t)nmax * W;
+  hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)pp3_stream(e);
+  HCHK(hipSetDevice(c->device));
+  // the root packs straight into its own slot of the destination; every other chunk is staged
+  float* mine;
+  if (root >= 0 && root == c->rank) {
+    mine = dst_dev + (size_t)c->rank * count;
+  } else {
+    if (c->pack_elems < count) {
+      HCHK(hipStreamSynchronize(s));  // (first call / growth only) the old buffer may be in flight
+      (void)hipFree(c->pack);
+      c->pack = nullptr;
+      HCHK(hipMalloc(&c->pack, count * sizeof(float)));
+      c->pack_elems = count;
+    }
+    mine = c->pack;
+  }
+  const unsigned blocks = (unsigned)((count + 255) / 256);
+  hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, (const float*)obs, (const float*)rew,
+                     (const float*)done, n, (int)D, nmax, mine);
+  HCHK(hipGetLastError());
+  if (root < 0) {
+    NCHK(R, R->AllGather(mine, dst_dev, count, ncclFloat32, c->comm, s));
+  } else if (c->world > 1) {
+    NCHK(R, R->GroupStart());
+    if (c->rank == root) {
+      for (int r = 0; r < c->world; r++)
+        if (r != root) {
+          ncclResult_t rr = R->Recv(dst_dev + (size_t)r * count, count, ncclFloat32, r, c->comm, s);
+          if (rr != ncclSuccess) { R->GroupEnd(); return cerr(PP3_ERR_COMM, std::string("ncclRecv: ") + R->GetErrorString(rr)); }
+        }
+    } else {
+      ncclResult_t rr = R->Send(mine, count, ncclFloat32, root, c->comm, s);
+      if (rr != ncclSuccess) { R->GroupEnd(); return cerr(PP3_ERR_COMM, std::string("ncclSend: ") + R->GetErrorString(rr)); }
+    }
+    NCHK(R, R->GroupEnd());
+  }
+  return PP3_OK;
+}
+
+int pp3_comm_allreduce(pp3_comm_t* c, const double* in, double* out, int32_t n, int32_t op) {
+  if (!c || !in || !out || n < 1 || n > 64) return cerr(PP3_ERR_ARG, "pp3_comm_allreduce: bad argument (n <= 64)");
+  const Rccl* R = rccl();
+  if (!R) return cerr(PP3_ERR_COMM, g_cerr);
+  HCHK(hipSetDevice(c->device));
+  HCHK(hipMemcpyAsync(c->red, in, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  NCHK(R, R->AllReduce(c->red, c->red, n, ncclFloat64, op == PP3_REDUCE_MAX ? ncclMax : ncclSum, c->comm, c->stream));
+  HCHK(hipMemcpyAsync(out, c->red, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HCHK(hipStreamSynchronize(c->stream));
+  return PP3_OK;
+}
+
+int pp3_comm_barrier(pp3_comm_t* c) {
+  double z = 0.0, o = 0.0;
+  return pp3_comm_allreduce(c, &z, &o, 1, PP3_REDUCE_SUM);
+}
+
+}  // extern "C"

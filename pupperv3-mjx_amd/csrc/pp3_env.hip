@@ -1763,6 +1763,7 @@ __device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m,
     else if (i < PP3_P_QACC) v = s.qfrc_act[i - PP3_P_QFRC_ACT];
     else if (i < PP3_P_NCON) v = s.qacc[i - PP3_P_QACC];
     else if (i == PP3_P_NCON) v = (float)s.ncon;
+    else if (i == PP3_P_NHIT) v = (float)s.nhit;
     else if (i < PP3_P_CON_GEOM) { const int c = i - PP3_P_CON_DIST; v = c < s.ncon ? s.con_dist[c] : 0.0f; }
     else if (i < PP3_P_SUBTREE_COM) {
       const int q = i - PP3_P_CON_GEOM, c = q / 2;
@@ -1849,6 +1850,9 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     if (l < PP3_EP_STRIDE) s.ep[l] = a.episode[(size_t)env * PP3_EP_STRIDE + l];
   }
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
+  // obs is updated in place (obs_in == obs_out): every history load of this half has returned
+  // before the first history store (for H >= 3 the shifted window overlaps the one it is read from)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (own)
 #pragma unroll
     for (int t = 0; t < OBS_MOVE; t++)
@@ -2251,8 +2255,7 @@ struct pp3_env {
   hipStream_t stream;
   DevModel* dmodel;
   float* state;
-  float* obs[2];
-  int obs_cur;
+  float* obs;  // [N][36H], updated in place by every step (stable pointer: pp3_field(PP3_F_OBS))
   float* reward;
   float* done;
   float* metrics;
@@ -2653,11 +2656,15 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
   d->resample_step = c->resample_velocity_step;
   d->term_step = c->early_termination_step_threshold;
   d->torso_body = c->torso_body;
+  if (c->torso_body < 1 || c->torso_body >= NB) return set_err(PP3_ERR_ARG, "torso body id out of range");
   for (int f = 0; f < 4; f++) {
     d->feet_site[f] = c->feet_site[f];
     d->lower_leg_body[f] = c->lower_leg_body[f];
     if (c->feet_site[f] < 0 || c->feet_site[f] >= mm->nsite) return set_err(PP3_ERR_ARG, "foot site not found");
+    if (c->lower_leg_body[f] < 1 || c->lower_leg_body[f] >= NB) return set_err(PP3_ERR_ARG, "lower-leg body id out of range");
   }
+  if (c->n_upper_leg_geoms < 0 || c->n_upper_leg_geoms > 16) return set_err(PP3_ERR_ARG, "n_upper_leg_geoms must be 0..16");
+  if (c->n_torso_geoms < 0 || c->n_torso_geoms > 8) return set_err(PP3_ERR_ARG, "n_torso_geoms must be 0..8");
   d->n_knee_geoms = c->n_upper_leg_geoms;
   for (int i = 0; i < c->n_upper_leg_geoms && i < 16; i++) d->knee_geoms[i] = c->upper_leg_geoms[i];
   d->n_torso_geoms = c->n_torso_geoms;
@@ -2756,8 +2763,7 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   HIPCHK(hipMalloc(&e->dmodel, sizeof(DevModel)));
   HIPCHK(hipMemcpy(e->dmodel, &hm, sizeof(DevModel), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&e->state, N * e->stride * sizeof(float)));
-  HIPCHK(hipMalloc(&e->obs[0], N * PP3_OBS_DIM * e->H * sizeof(float)));
-  HIPCHK(hipMalloc(&e->obs[1], N * PP3_OBS_DIM * e->H * sizeof(float)));
+  HIPCHK(hipMalloc(&e->obs, N * PP3_OBS_DIM * e->H * sizeof(float)));
   HIPCHK(hipMalloc(&e->reward, N * sizeof(float)));
   HIPCHK(hipMalloc(&e->done, N * sizeof(float)));
   HIPCHK(hipMalloc(&e->metrics, N * PP3_NMETRIC * sizeof(float)));
@@ -2765,8 +2771,7 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   HIPCHK(hipMalloc(&e->pipe, N * PP3_PIPE_STRIDE * sizeof(float)));
   HIPCHK(hipMalloc(&e->action, N * PP3_NU * sizeof(float)));
   HIPCHK(hipMemset(e->state, 0, N * e->stride * sizeof(float)));
-  HIPCHK(hipMemset(e->obs[0], 0, N * PP3_OBS_DIM * e->H * sizeof(float)));
-  HIPCHK(hipMemset(e->obs[1], 0, N * PP3_OBS_DIM * e->H * sizeof(float)));
+  HIPCHK(hipMemset(e->obs, 0, N * PP3_OBS_DIM * e->H * sizeof(float)));
   HIPCHK(hipMemset(e->pipe, 0, N * PP3_PIPE_STRIDE * sizeof(float)));
   HIPCHK(hipMemset(e->action, 0, N * PP3_NU * sizeof(float)));
   HIPCHK(hipEventCreate(&e->ev0));
@@ -2779,7 +2784,7 @@ int pp3_destroy(pp3_env_t* e) {
   if (!e) return PP3_OK;
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
-  void* bufs[] = {e->dmodel, e->state, e->obs[0], e->obs[1], e->reward, e->done, e->metrics, e->dr, e->pipe, e->action,
+  void* bufs[] = {e->dmodel, e->state, e->obs, e->reward, e->done, e->metrics, e->dr, e->pipe, e->action,
                   e->episode, e->first_state, e->first_obs, e->terrain};
   for (void* b : bufs) (void)hipFree(b);
   (void)hipEventDestroy(e->ev0);
@@ -2800,7 +2805,7 @@ int pp3_reset(pp3_env_t* e, const uint32_t* keys_dev, const uint8_t* mask_dev, v
   ResetArgs a;
   a.m = e->dmodel;
   a.state = e->state;
-  a.obs = e->obs[e->obs_cur];
+  a.obs = e->obs;
   a.reward = e->reward;
   a.done = e->done;
   a.metrics = e->metrics;
@@ -2824,8 +2829,8 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   StepArgs a;
   a.m = e->dmodel;
   a.state = e->state;
-  a.obs_in = e->obs[e->obs_cur];
-  a.obs_out = e->obs[e->obs_cur ^ 1];
+  a.obs_in = e->obs;  // in place: each half-wave loads its env's history before storing it
+  a.obs_out = e->obs;
   a.actions = actions_dev;
   a.reward = e->reward;
   a.done = e->done;
@@ -2840,7 +2845,6 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   else hipLaunchKernelGGL(env_step_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
   HIPCHK(hipGetLastError());
-  e->obs_cur ^= 1;
   return PP3_OK;
 }
 
@@ -2857,7 +2861,7 @@ int pp3_set_auto_reset(pp3_env_t* e, int32_t episode_length) {
     // until the next pp3_reset the current state is the "first" state
     HIPCHK(hipMemcpy2DAsync(e->first_state, sizeof(float) * PP3_FIRST_STRIDE, e->state, sizeof(float) * e->stride,
                             sizeof(float) * PP3_FIRST_STRIDE, e->N, hipMemcpyDeviceToDevice, e->stream));
-    HIPCHK(hipMemcpyAsync(e->first_obs, e->obs[e->obs_cur], sizeof(float) * (size_t)e->N * PP3_OBS_DIM * e->H,
+    HIPCHK(hipMemcpyAsync(e->first_obs, e->obs, sizeof(float) * (size_t)e->N * PP3_OBS_DIM * e->H,
                           hipMemcpyDeviceToDevice, e->stream));
   }
   e->episode_length = episode_length > 0 ? episode_length : 0;
@@ -2949,7 +2953,7 @@ int pp3_field(pp3_env_t* e, int32_t field, void** ptr, int64_t* elems) {
   void* p = nullptr;
   switch (field) {
     case PP3_F_STATE: p = e->state; n = e->stride; break;
-    case PP3_F_OBS: p = e->obs[e->obs_cur]; n = (int64_t)PP3_OBS_DIM * e->H; break;
+    case PP3_F_OBS: p = e->obs; n = (int64_t)PP3_OBS_DIM * e->H; break;
     case PP3_F_REWARD: p = e->reward; n = 1; break;
     case PP3_F_DONE: p = e->done; n = 1; break;
     case PP3_F_METRICS: p = e->metrics; n = PP3_NMETRIC; break;

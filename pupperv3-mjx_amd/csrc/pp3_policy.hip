@@ -202,6 +202,7 @@ int pp3_policy_act(pp3_policy_t* p, const float* obs_dev, int64_t obs_stride, in
   if (!p || !obs_dev || !actions_dev) return perr(PP3_ERR_ARG, "pp3_policy_act: null argument");
   if (n <= 0) return PP3_OK;
   if (obs_stride < p->net.in_dim) return perr(PP3_ERR_ARG, "pp3_policy_act: observation row shorter than in_dim");
+  if (action_stride < p->net.out_dim) return perr(PP3_ERR_ARG, "pp3_policy_act: action row shorter than out_dim");
   PHIP(hipSetDevice(p->device));
   hipLaunchKernelGGL(mlp_kernel, dim3((n + TILE - 1) / TILE), dim3(64 * NWAVE), 0, (hipStream_t)stream, p->net,
                      obs_dev, (int)obs_stride, actions_dev, (int)action_stride, n);

@@ -30,6 +30,11 @@ FIRST_STRIDE = 55
 P_XPOS, P_XQUAT, P_XD_VEL, P_XD_ANG = 0, 39, 91, 130
 P_SITE_XPOS, P_QFRC_ACT, P_QACC, P_NCON = 169, 181, 199, 217
 P_CON_DIST, P_CON_GEOM, P_SUBTREE_COM, P_SENSOR, PIPE_STRIDE = 218, 234, 266, 272, 304
+P_NHIT = 269  # penetrating pairs before the contact cap
+
+ERR_ARG, ERR_MODEL, ERR_HIP, ERR_NOMEM, ERR_COMM = 1, 2, 3, 4, 5
+COMM_ID_BYTES = 128  # PP3_COMM_ID_BYTES (ncclUniqueId)
+REDUCE_SUM, REDUCE_MAX = 0, 1
 
 DR_FRICTION, DR_KP, DR_KD, DR_BASE_IPOS, DR_INERTIA, DR_MASS = 0, 1, 2, 3, 6, 48
 

@@ -68,12 +68,25 @@ def load() -> C.CDLL:
     L.pp3_set_terrain.argtypes = [vp, vp, i32]
     L.pp3_terrain_slots.argtypes = [vp]
     L.pp3_terrain_slots.restype = i32
+    # multi-GPU (pp3_comm.hip; RCCL is dlopen'ed by the library on first use)
+    L.pp3_comm_unique_id.argtypes = [vp]
+    L.pp3_comm_init.argtypes = [vp, i32, i32, i32, C.POINTER(vp)]
+    L.pp3_comm_destroy.argtypes = [vp]
+    L.pp3_comm_rank.argtypes = [vp]
+    L.pp3_comm_rank.restype = i32
+    L.pp3_comm_world.argtypes = [vp]
+    L.pp3_comm_world.restype = i32
+    L.pp3_comm_last_error.restype = C.c_char_p
+    L.pp3_gather.argtypes = [vp, vp, i32, i32, vp, vp]
+    L.pp3_comm_allreduce.argtypes = [vp, vp, vp, i32, i32]
+    L.pp3_comm_barrier.argtypes = [vp]
     for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
                  "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
                  "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
                  "pp3_set_auto_reset", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy",
-                 "pp3_set_terrain"):
+                 "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
+                 "pp3_comm_allreduce", "pp3_comm_barrier"):
         getattr(L, name).restype = C.c_int
     if L.pp3_abi_version() != _abi.ABI_VERSION:
         raise PupperHipError("ABI version mismatch between libpupper_hip.so and pupperv3_mjx/_abi.py")
@@ -89,6 +102,12 @@ def check(rc: int) -> None:
         raise PupperHipError(f"pupper_hip error {rc}: {msg}")
 
 
+def check_comm(rc: int) -> None:
+    if rc != 0:
+        msg = load().pp3_comm_last_error().decode(errors="replace")
+        raise PupperHipError(f"pupper_hip comm error {rc}: {msg}")
+
+
 EXPORTED_SYMBOLS = (
     "pp3_abi_version", "pp3_struct_size", "pp3_last_error", "pp3_device_count", "pp3_create", "pp3_destroy",
     "pp3_num_envs", "pp3_state_stride", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
@@ -97,6 +116,8 @@ EXPORTED_SYMBOLS = (
     "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_set_auto_reset",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
     "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
+    "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_comm_rank", "pp3_comm_world",
+    "pp3_comm_last_error", "pp3_gather", "pp3_comm_allreduce", "pp3_comm_barrier",
 )
 
 

@@ -415,6 +415,7 @@ class PupperV3Env:
             ps.sensordata = p[:, _abi.P_SENSOR:_abi.P_SENSOR + self.sys_model.struct.nsensordata]
         st = State(pipeline_state=ps, obs=obs, reward=rew, done=done, metrics=metrics, info=info)
         st._record = rec
+        st._metrics_raw = met  # [N][19]: total_dist, then the scaled terms in _abi.REWARD_NAMES order
         if single:
             st = _squeeze(st)
         return st
@@ -476,6 +477,7 @@ def _squeeze(st: State) -> State:
     out = State(pipeline_state=ps2, obs=sq(st.obs), reward=sq(st.reward), done=sq(st.done),
                 metrics=sq(st.metrics), info=sq(st.info))
     out._record = st._record
+    out._metrics_raw = st._metrics_raw
     return out
 
 

@@ -146,6 +146,8 @@ class DevicePolicy:
     def act_env(self, env, actions_dev: int, stream=None) -> None:
         """actions[N][12] = policy(env's current observation buffer)."""
         from . import _abi
+        if self.out_dim != _abi.NU:
+            raise ValueError(f"act_env needs a policy with {_abi.NU} outputs (the action), this one has {self.out_dim}")
         obs_ptr, obs_n = env.device_field(_abi.F_OBS)
         if stream is None:  # order with the env's kernels
             stream = env._L.pp3_stream(env._h)

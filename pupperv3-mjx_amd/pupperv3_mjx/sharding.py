@@ -1,15 +1,23 @@
-"""Env sharding across GPUs (one process per GPU) and the optional learner gather.
+"""Env sharding across GPUs (one process per GPU) and the learner-batch collective.
 
 SURVEY.md 8(e): envs are independent, so a global batch of G envs is cut into contiguous
 per-rank shards with no collective inside the step.  Env i of the global batch gets the same
 PRNG key (``jax.random.split(PRNGKey(seed), G)[i]``) whatever the world size, so a sharded run
 reproduces the single-GPU run env-for-env.  The only collective is the optional per-step
-gather of ``obs | reward | done`` to every rank (RCCL all_gather over xGMI on GPUs; gloo on CPU
-in tests), sized for uneven shards by padding to the largest shard.
+hand-over of ``obs | reward | done`` to the learner: ``Comm.gather`` -> ``pp3_gather`` (RCCL over
+xGMI, on the env's stream, no host sync; include/pupper_hip.h).  No torch anywhere: the RCCL
+communicator id is exchanged by a file rendezvous on the node (``rendezvous_id``).
+
+Gathered layout (``pp3_gather``): rank r's ``nmax`` rows of width D + 2 at row r * nmax, rows past
+the rank's env count zero; ``pack_rows`` is its numpy statement, ``unpack_gathered`` drops the
+padding and returns the global [G, D] / [G] / [G] batch in env-id order.
 """
 from __future__ import annotations
 
-from typing import Tuple
+import ctypes as C
+import os
+import time
+from typing import Callable, Optional, Tuple
 
 import numpy as np
 
@@ -35,23 +43,140 @@ def shard_keys(seed: int, global_envs: int, world: int, rank: int, partitionable
     return np.ascontiguousarray(keys[start:start + count])
 
 
-def gather_batch(obs, reward, done, global_envs: int, group=None):
-    """All-gather this rank's (obs [n, D], reward [n], done [n]) torch tensors into global
-    [G, D] / [G] / [G] tensors on every rank (torch.distributed; RCCL or gloo)."""
-    import torch
-    import torch.distributed as dist
+def max_shard(global_envs: int, world: int) -> int:
+    """Rows every rank contributes to the gather (the largest shard: rank 0's)."""
+    return shard_bounds(global_envs, world, 0)[1]
 
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    start, n = shard_bounds(global_envs, world, rank)
-    nmax = shard_bounds(global_envs, world, 0)[1]
-    D = obs.shape[1]
-    local = torch.zeros((nmax, D + 2), dtype=torch.float32, device=obs.device)
-    local[:n, :D] = obs
-    local[:n, D] = reward
-    local[:n, D + 1] = done
-    full = torch.empty((world * nmax, D + 2), dtype=torch.float32, device=obs.device)
-    dist.all_gather_into_tensor(full, local, group=group)
+
+def pack_rows(obs, reward, done, nmax: int) -> np.ndarray:
+    """numpy statement of pp3_comm.hip's pack_kernel: [nmax, D + 2] = obs | reward | done, zero rows
+    past the shard's env count."""
+    obs = np.asarray(obs, dtype=np.float32)
+    n, D = obs.shape
+    out = np.zeros((nmax, D + 2), dtype=np.float32)
+    out[:n, :D] = obs
+    out[:n, D] = np.asarray(reward, dtype=np.float32).reshape(n)
+    out[:n, D + 1] = np.asarray(done, dtype=np.float32).reshape(n)
+    return out
+
+
+def unpack_gathered(full, global_envs: int, world: int):
+    """[world * nmax, D + 2] gathered rows -> (obs [G, D], reward [G], done [G]) in global env order."""
+    full = np.asarray(full)
+    nmax = max_shard(global_envs, world)
     rows = [full[r * nmax:r * nmax + shard_bounds(global_envs, world, r)[1]] for r in range(world)]
-    out = torch.cat(rows, 0)
+    out = np.concatenate(rows, 0)
+    D = out.shape[1] - 2
     return out[:, :D], out[:, D], out[:, D + 1]
+
+
+# ------------------------------------------------------------------------------ rendezvous
+def _rdzv_path(tag: str) -> str:
+    """Per-launch file name on the node.  Explicit PP3_RDZV_FILE wins (e.g. a shared file system
+    for several nodes); under torch.distributed.run every worker of one launch has the same
+    parent (the elastic agent) and MASTER_PORT, which key the file."""
+    explicit = os.environ.get("PP3_RDZV_FILE")
+    if explicit:
+        return explicit + tag
+    base = os.environ.get("PP3_RDZV_DIR", "/tmp")
+    port = os.environ.get("MASTER_PORT", "0")
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "none")
+    return os.path.join(base, f"pp3_rdzv_{os.getppid()}_{port}_{run}{tag}.bin")
+
+
+def rendezvous_id(rank: int, world: int, make_id: Callable[[], bytes], tag: str = "",
+                  timeout_s: float = 120.0) -> bytes:
+    """Rank 0 creates the communicator id (``make_id``) and publishes it atomically in a file on
+    the node; the other ranks poll for it.  Returns the id on every rank."""
+    path = _rdzv_path(tag)
+    if rank == 0:
+        blob = bytes(make_id())
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(blob)
+        os.replace(tmp, path)  # atomic publish
+        return blob
+    t0 = time.monotonic()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                blob = f.read()
+            if blob:
+                return blob
+        except FileNotFoundError:
+            pass
+        if time.monotonic() - t0 > timeout_s:
+            raise TimeoutError(f"rank {rank}: no communicator id at {path} after {timeout_s:.0f} s")
+        time.sleep(0.01)
+
+
+def rendezvous_cleanup(tag: str = "") -> None:
+    try:
+        os.remove(_rdzv_path(tag))
+    except FileNotFoundError:
+        pass
+
+
+# ------------------------------------------------------------------------------ RCCL comm
+class Comm:
+    """One rank of the env-sharded job: an RCCL communicator created through the C ABI
+    (pp3_comm_init), the learner gather, and the host-blocking barrier / reductions the bench's
+    max-over-ranks timing uses."""
+
+    def __init__(self, rank: int, world: int, device: int, tag: str = ""):
+        from . import _abi, _lib
+        self._lib = _lib
+        self._L = L = _lib.load()
+        self.rank, self.world, self.device = int(rank), int(world), int(device)
+
+        def make_id():
+            buf = (C.c_uint8 * _abi.COMM_ID_BYTES)()
+            _lib.check_comm(L.pp3_comm_unique_id(buf))
+            return bytes(buf)
+
+        uid = rendezvous_id(self.rank, self.world, make_id, tag)
+        ubuf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _lib.check_comm(L.pp3_comm_init(ubuf, self.rank, self.world, self.device, C.byref(h)))
+        self._h = h
+        self._tag = tag
+        self.barrier()  # every rank has read the id: rank 0 may remove the file
+        if self.rank == 0:
+            rendezvous_cleanup(tag)
+
+    @classmethod
+    def from_env(cls, device: Optional[int] = None) -> "Comm":
+        """RANK / WORLD_SIZE / LOCAL_RANK as set by torch.distributed.run (or any launcher)."""
+        rank = int(os.environ.get("RANK", "0"))
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        dev = int(os.environ.get("LOCAL_RANK", "0")) if device is None else device
+        return cls(rank, world, dev)
+
+    def gather(self, env, nmax: int, dst_dev: Optional[int], root: int = 0, stream: Optional[int] = None) -> None:
+        """Learner batch of every rank's shard into dst_dev (see module doc); root < 0 = all-gather."""
+        self._lib.check_comm(self._L.pp3_gather(self._h, env._h, int(nmax), int(root),
+                                                C.c_void_p(dst_dev) if dst_dev else None,
+                                                C.c_void_p(stream) if stream else None))
+
+    def allreduce(self, values, op: str = "max") -> np.ndarray:
+        from . import _abi
+        v = np.ascontiguousarray(values, dtype=np.float64).ravel()
+        out = np.empty_like(v)
+        self._lib.check_comm(self._L.pp3_comm_allreduce(
+            self._h, v.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p), v.size,
+            _abi.REDUCE_MAX if op == "max" else _abi.REDUCE_SUM))
+        return out
+
+    def barrier(self) -> None:
+        self._lib.check_comm(self._L.pp3_comm_barrier(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.pp3_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,68 @@
+"""The multi-GPU collective through the C ABI on one GPU.
+
+pp3_gather on a one-rank RCCL communicator: the device pack of obs | reward | done (with padding
+rows past the shard) must equal sharding.pack_rows of the env's own fields, for the gather to
+a root and for the all-gather; the reductions the bench's max-over-ranks timing uses must
+return their inputs.  (Several ranks need several GPUs -- RCCL allows one rank per device --
+so the N > 1 exchange itself is covered by the gloo test in test_sharding.py and the driver's
+8-GPU bench.)
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import common
+from pupperv3_mjx import _abi, _lib, sharding
+from pupperv3_mjx.environment import PupperV3Env, make_keys
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm(require_gpu, tmp_path_factory):
+    import os
+    os.environ["PP3_RDZV_DIR"] = str(tmp_path_factory.mktemp("rdzv"))
+    c = sharding.Comm(0, 1, 0, tag="_test")
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("root", [0, -1])
+def test_gather_packs_learner_rows(comm, root):
+    n, nmax = 37, 40
+    env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=n)
+    try:
+        st = env.reset(make_keys(3, n))
+        st = env.step(st, np.random.RandomState(0).uniform(-1, 1, size=(n, 12)).astype(np.float32))
+        width = env.observation_size + 2
+        dst = _lib.DeviceBuffer(nmax * width * 4, env.device)
+        # poison the destination so the padding rows are checked as written, not assumed
+        dst.upload(np.full(nmax * width, np.nan, np.float32))
+        comm.gather(env, nmax, dst.ptr.value, root=root)
+        env.synchronize()
+        got = np.empty((nmax, width), np.float32)
+        dst.download(got)
+        dst.free()
+        np.testing.assert_array_equal(got, sharding.pack_rows(st.obs, st.reward, st.done, nmax))
+        o, r, d = sharding.unpack_gathered(got, n, 1)
+        np.testing.assert_array_equal(o, st.obs)
+    finally:
+        env.close()
+
+
+def test_gather_rejects_short_nmax(comm):
+    env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=8)
+    try:
+        env.reset(make_keys(0, 8))
+        with pytest.raises(_lib.PupperHipError):
+            comm.gather(env, 7, None, root=0)
+    finally:
+        env.close()
+
+
+def test_allreduce_and_barrier(comm):
+    np.testing.assert_array_equal(comm.allreduce([1.5, -2.0, 3.25], "max"), [1.5, -2.0, 3.25])
+    np.testing.assert_array_equal(comm.allreduce([1.5, -2.0], "sum"), [1.5, -2.0])
+    comm.barrier()
+    assert comm._L.pp3_comm_world(comm._h) == 1 and comm._L.pp3_comm_rank(comm._h) == 0

@@ -2,9 +2,12 @@
 
 Each rank takes its contiguous shard of a global batch (pupperv3_mjx.sharding), steps it with
 the CPU oracle (the GPU kernel is not available here; the sharding logic is the same code the
-bench uses), and the per-step learner gather (sharding.gather_batch) reassembles obs / reward /
-done.  The gathered batch must equal a single-process run of the whole batch bit-for-bit:
-envs are independent and keys depend only on the global env id.
+bench uses), packs its learner rows exactly as pp3_gather's device pack does
+(sharding.pack_rows), and a gloo all-gather stands in for the RCCL collective (torch is used by
+this test only, as the CPU transport; the product path is torch-free).  sharding.unpack_gathered
+must then give a single-process run of the whole batch bit-for-bit: envs are independent and
+keys depend only on the global env id.  The communicator-id rendezvous (file based, no torch)
+runs in real processes too.
 """
 import os
 import socket
@@ -53,11 +56,14 @@ def _worker(rank, world, port, path, ret):
         per_step = _rollout(model, cfg, keys, acts)
         if rank == 0:
             ret["gathered"] = []
+        nmax = sharding.max_shard(G_ENVS, world)
         for obs, rew, done in per_step:
-            o, r, d = sharding.gather_batch(torch.from_numpy(obs).float(), torch.from_numpy(rew).float(),
-                                            torch.from_numpy(done).float(), G_ENVS)
+            local = torch.from_numpy(sharding.pack_rows(obs, rew, done, nmax))
+            full = torch.empty((world * nmax, local.shape[1]), dtype=torch.float32)
+            dist.all_gather_into_tensor(full, local)
+            o, r, d = sharding.unpack_gathered(full.numpy(), G_ENVS, world)
             if rank == 0:
-                ret["gathered"] = ret["gathered"] + [(o.numpy(), r.numpy(), d.numpy())]
+                ret["gathered"] = ret["gathered"] + [(o, r, d)]
     finally:
         dist.destroy_process_group()
 
@@ -94,3 +100,50 @@ def test_two_rank_gloo_gather_matches_single_process(tmp_path):
         np.testing.assert_array_equal(go, ro.astype(np.float32))
         np.testing.assert_array_equal(gr, rr.astype(np.float32))
         np.testing.assert_array_equal(gd, rd.astype(np.float32))
+
+
+def _rdzv_worker(rank, world, d, ret):
+    os.environ["PP3_RDZV_DIR"] = d
+    os.environ["MASTER_PORT"] = "4242"
+    blob = sharding.rendezvous_id(rank, world, lambda: os.urandom(128), timeout_s=30)
+    ret[rank] = blob
+
+
+def test_rendezvous_id_file_exchange(tmp_path):
+    """Rank 0's 128-byte communicator id reaches every rank (the RCCL init input), no torch."""
+    import multiprocessing as mpc
+    with mpc.Manager() as mgr:
+        ret = mgr.dict()
+        ps = [mpc.Process(target=_rdzv_worker, args=(r, 3, str(tmp_path), ret)) for r in (1, 2, 0)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(60)
+            assert p.exitcode == 0
+        blobs = [ret[r] for r in range(3)]
+    assert len(blobs[0]) == 128 and blobs[0] == blobs[1] == blobs[2]
+
+
+def test_pack_unpack_ragged():
+    rs = np.random.RandomState(0)
+    G, world, D = 11, 4, 72
+    obs = rs.normal(size=(G, D)).astype(np.float32)
+    rew, done = rs.uniform(size=G).astype(np.float32), (rs.uniform(size=G) < 0.3).astype(np.float32)
+    nmax = sharding.max_shard(G, world)
+    full = np.concatenate([sharding.pack_rows(obs[s:s + n], rew[s:s + n], done[s:s + n], nmax)
+                           for s, n in (sharding.shard_bounds(G, world, r) for r in range(world))])
+    assert full.shape == (world * nmax, D + 2)
+    o, r, d = sharding.unpack_gathered(full, G, world)
+    np.testing.assert_array_equal(o, obs)
+    np.testing.assert_array_equal(r, rew)
+    np.testing.assert_array_equal(d, done)
+
+
+def test_sharding_module_is_torch_free():
+    import ast
+    import inspect
+    src = inspect.getsource(sharding)
+    names = {a.name for n in ast.walk(ast.parse(src)) if isinstance(n, (ast.Import, ast.ImportFrom))
+             for a in n.names}
+    mods = {n.module for n in ast.walk(ast.parse(src)) if isinstance(n, ast.ImportFrom) and n.module}
+    assert not any(x.split(".")[0] == "torch" for x in names | mods)
