@@ -174,3 +174,20 @@ class TermStats:
     @staticmethod
     def failures(errs):
         return {k: (e, tol) for k, (e, tol) in errs.items() if not e <= tol}
+
+
+def env_with_model(path, model_struct, n, **kw):
+    """A device env built from an edited model struct (known-answer tests on modified physics):
+    the env config comes from the reference fixture kwargs, the model from `model_struct`."""
+    import ctypes as C
+    import common
+    e = PupperV3Env(**common.fixture_kwargs(path, **kw), num_envs=n, create_device=False)
+    L = _lib.load()
+    h = C.c_void_p()
+    _lib.check(L.pp3_create(C.byref(model_struct), C.byref(e.config_struct), n, 0, C.byref(h)))
+    e._h, e._L = h, L
+    _lib.check(L.pp3_set_pipeline_output(h, 1))
+    e._keys_buf = _lib.DeviceBuffer(n * 8, 0)
+    e._act_buf = _lib.DeviceBuffer(n * _abi.NU * 4, 0)
+    e._dr_buf = None
+    return e
