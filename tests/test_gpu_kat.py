@@ -45,7 +45,9 @@ def test_kernel_frictionloss_creep(require_gpu):
 
 
 def test_kernel_frictionloss_slip(require_gpu):
-    m, ctrl, out = _run(require_gpu, [0.25, -0.25, 0.4, -0.18], [2, 8])
+    # |tau| <= 0.25: the parent hinges' reaction stays below their frictionloss, so they hold and the
+    # knee alone accelerates (from |tau| ~ 0.28 the parents slip too and the M_jj law no longer applies)
+    m, ctrl, out = _run(require_gpu, [0.25, -0.25, 0.2, -0.18], [2, 8])
     v1, v2 = out[0][1][:, KNEE], out[1][1][:, KNEE]
     acc = (v2 - v1) / (6 * m.timestep)
     q = np.zeros(19)
@@ -56,3 +58,4 @@ def test_kernel_frictionloss_slip(require_gpu):
     vm = 0.5 * (v1 + v2)
     expect = (tau - np.sign(tau) * m.dof_frictionloss[KNEE] - m.dof_damping[KNEE] * vm) / Mkk
     np.testing.assert_allclose(acc, expect, rtol=1.5e-2)
+    assert np.all(np.abs(out[1][1][:, 6:8]).max(axis=1) < 1e-2 * np.abs(v2))  # parents held

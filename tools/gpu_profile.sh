@@ -4,7 +4,7 @@
 #   each under its own time limit; stops at the first failure.
 set -e
 TAG=${1:-prof}
-ARGS=${2:---steps 50 --warmup 5 --no-cpu-baseline --no-latency-floor}
+ARGS=${2:---steps 50 --warmup 5 --no-cpu-baseline --no-latency-floor --no-extras}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
