@@ -82,7 +82,8 @@ struct alignas(16) Shared {
   float M[NV][NV + 1];
   float gxpos[NROBOT_GEOM][3];
   float foot_xpos[4][3];
-  float qfrc_smooth[NV], qfrc_act[NV], qacc_smooth[NV], Ma[NV], grad[NV], search[NV], dofD[NV];
+  alignas(16) float search[20];  // (read as b128 words by mrow_dot_reg)
+  float qfrc_smooth[NV], qfrc_act[NV], qacc_smooth[NV], grad[NV], dofD[NV];
   // contacts
   int ncon, nhit, nl;
   int con_pair[NC], con_sup[NC];
@@ -95,10 +96,6 @@ struct alignas(16) Shared {
   float lim_sgn[NLMAX];
   float efc_D[NEFC], efc_R[NEFC], efc_aref[NEFC], efc_force[NEFC];
   Scratch<NC> x;
-#ifdef PP3_PHASE_PROF
-  uint64_t prof[22];
-  uint64_t prof_t;
-#endif
 };
 
 // A workgroup is ONE wave and LDS executes a wave's instructions in issue order, so a lane's
@@ -143,17 +140,35 @@ __device__ __forceinline__ LaneRec<N> fetch_rec(const LaneTab<N>& t, int l) {
 }
 __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 
-// Diagnostic build only (-DPP3_PHASE_PROF): per-phase s_memtime deltas summed over all envs.
+// Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-cycle deltas summed over all
+// waves.  A stamp is one s_memtime (its lgkmcnt wait drains the LDS reads in flight) and two VALU:
+// lane k of a per-wave register accumulates phase k's cycles, one global atomic per lane at the
+// end of the launch (gfx950 has no SHADER_CYCLES hwreg).
 #ifdef PP3_PHASE_PROF
 constexpr int NPROF = 22;  // 0..18 phase cycles, 19 line-search evaluations per wave (max of its two envs), 20 per env
 __device__ unsigned long long g_prof[NPROF];
-#define PHASE(k)                                                          \
-  do {                                                                    \
-    asm volatile("; PP3PHASE " #k);                                       \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();                     \
-    if (l == 0) { s.prof[k] += t_ - s.prof_t; s.prof_t = t_; }            \
+struct Prof {
+  uint32_t t, acc;
+};
+__device__ __forceinline__ uint32_t shader_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
+#define PROF_PARAM , Prof* pf
+#define PROF_ARG , pf
+#define PROF_NULL , (Prof*)nullptr
+#define PROF_ADD(k, v) do { if (pf) pf->acc += ((int)(threadIdx.x) == (k)) ? (uint32_t)(v) : 0u; } while (0)
+#define PHASE(k)                                                            \
+  do {                                                                      \
+    if (pf) {                                                               \
+      asm volatile("; PP3PHASE " #k);                                       \
+      const uint32_t t_ = shader_cycles();                                  \
+      pf->acc += ((int)(threadIdx.x) == (k)) ? (t_ - pf->t) : 0u;         \
+      pf->t = t_;                                                           \
+    }                                                                       \
   } while (0)
 #else
+#define PROF_PARAM
+#define PROF_ARG
+#define PROF_NULL
+#define PROF_ADD(k, v) do { } while (0)
 #define PHASE(k) do { } while (0)
 #endif
 
@@ -834,12 +849,19 @@ __device__ __forceinline__ void hess_acc_p(float (&a)[NV], const float (&J)[3][N
   for (int j = J0; j < J1; j++) a[npos(j)] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
 }
 
-// row l (< NV) of M dotted with the LDS vector x, ascending j from 0
-template <int NC>
-__device__ __forceinline__ float mrow_dot(const Shared<NC>& s, int l, const float* x) {
+// (M x)[pnat(l)] from this lane's permuted M row held in registers (mrow[j] = M[pnat(l)][pnat(j)])
+// and the LDS vector x (16-byte aligned, read as broadcast b128 words): no per-element LDS round
+// trip.  The sum runs in permuted column order.
+__device__ __forceinline__ float mrow_dot_reg(const float (&mrow)[NV], const float* x) {
+  float xv[20];
+#pragma unroll
+  for (int q = 0; q < 20; q += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(x + q);
+    xv[q] = v.x; xv[q + 1] = v.y; xv[q + 2] = v.z; xv[q + 3] = v.w;
+  }
   float acc = 0;
 #pragma unroll
-  for (int j = 0; j < NV; j++) acc += s.M[l][j] * x[j];
+  for (int j = 0; j < NV; j++) acc += mrow[j] * xv[pnat(j)];
   return acc;
 }
 
@@ -848,21 +870,26 @@ __device__ __forceinline__ float mrow_dot(const Shared<NC>& s, int l, const floa
 // evaluated with clamped indices and the row's value selected, instead of three divergent
 // branches per call.  Contact rows: support = base + one leg (base-only contacts: that leg's
 // columns are zero), in ascending column order, so skipping exact zeros leaves the sums
-// bit-identical; a leg-leg contact anywhere in the wave (rare) takes full rows.
+// bit-identical; a leg-leg contact anywhere in the wave (rare) takes full rows.  nl / ncon come
+// from the caller's registers, so the row's metadata (limit dof and sign, contact support and
+// friction) is one round of independent LDS loads, and the sparse path's J entries and vector
+// entries are a second round, pinned so they issue back to back and retire with one wait.
+typedef float v2f __attribute__((ext_vector_type(2)));
 template <int NC, int K>
-__device__ __forceinline__ void row_dotk(const Shared<NC>& s, int r, const float* const (&xs)[K], float (&out)[K]) {
-  const int nl = s.nl, ncon = s.ncon;
+__device__ __forceinline__ void row_dotk(const Shared<NC>& s, int r, int nl, int ncon, const float* const (&xs)[K],
+                                         float (&out)[K]) {
   const bool isf = r < NFR, isl = !isf && r < NFR + nl;
   const int li = isl ? r - NFR : 0;
-  const int ld = s.lim_dof[li];
-  const float ls = s.lim_sgn[li];
-  const int col1 = isf ? 6 + r : (isl ? ld : 0);  // (never an uninitialised index)
-  const float sg1 = isf ? 1.0f : ls;
   const int e0 = r - NFR - nl, e = e0 < 0 ? 0 : e0;
   const int c = (e >> 2) < NC ? (e >> 2) : NC - 1, ed = e & 3, t = 1 + (ed >> 1);
   const bool isc = !isf && !isl && (e0 >> 2) < ncon;
   const float sg = (ed & 1) ? -1.0f : 1.0f;
+  const int ld = s.lim_dof[li];
+  const float ls = s.lim_sgn[li];
   const int sup = s.con_sup[c];
+  const float mu = s.con_mu[c];
+  const int col1 = isf ? 6 + r : (isl ? ld : 0);  // (never an uninitialised index)
+  const float sg1 = isf ? 1.0f : ls;
   float a[K], b[K];
 #pragma unroll
   for (int k = 0; k < K; k++) { a[k] = 0.0f; b[k] = 0.0f; }
@@ -875,33 +902,56 @@ __device__ __forceinline__ void row_dotk(const Shared<NC>& s, int r, const float
     }
   } else {
     const int o = 6 + 3 * (sup & 3);
+    v2f jj[9];      // (J normal, J tangent) of the row's 9 support columns
+    float xv[K][9];
+    float x1[K];    // the single-dof rows' entry
 #pragma unroll
     for (int i = 0; i < 9; i++) {
       const int col = i < 6 ? i : o + i - 6;
-      const float j0 = s.Jc[c][0][col], jt = s.Jc[c][t][col];
+      jj[i] = v2f{s.Jc[c][0][col], s.Jc[c][t][col]};
 #pragma unroll
-      for (int k = 0; k < K; k++) { a[k] += j0 * xs[k][col]; b[k] += jt * xs[k][col]; }
+      for (int k = 0; k < K; k++) xv[k][i] = xs[k][col];
     }
+#pragma unroll
+    for (int k = 0; k < K; k++) x1[k] = xs[k][col1];
+    if constexpr (K == 1) {
+      PIN("+v"(jj[0]), "+v"(jj[1]), "+v"(jj[2]), "+v"(jj[3]), "+v"(jj[4]), "+v"(jj[5]), "+v"(jj[6]), "+v"(jj[7]),
+          "+v"(jj[8]), "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[0][4]),
+          "+v"(xv[0][5]), "+v"(xv[0][6]), "+v"(xv[0][7]), "+v"(xv[0][8]), "+v"(x1[0]));
+    } else {
+      static_assert(K == 2, "row_dotk: K = 1 or 2");
+      PIN("+v"(jj[0]), "+v"(jj[1]), "+v"(jj[2]), "+v"(jj[3]), "+v"(jj[4]), "+v"(jj[5]), "+v"(jj[6]), "+v"(jj[7]),
+          "+v"(jj[8]), "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[0][4]),
+          "+v"(xv[0][5]), "+v"(xv[0][6]), "+v"(xv[0][7]), "+v"(xv[0][8]), "+v"(xv[1][0]), "+v"(xv[1][1]),
+          "+v"(xv[1][2]), "+v"(xv[1][3]), "+v"(xv[1][4]), "+v"(xv[1][5]), "+v"(xv[1][6]), "+v"(xv[1][7]),
+          "+v"(xv[1][8]), "+v"(x1[0]), "+v"(x1[1]));
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++)
+#pragma unroll
+      for (int k = 0; k < K; k++) { a[k] += jj[i].x * xv[k][i]; b[k] += jj[i].y * xv[k][i]; }
+#pragma unroll
+    for (int k = 0; k < K; k++) out[k] = (isf || isl) ? sg1 * x1[k] : a[k] + sg * mu * b[k];
+    return;
   }
-  const float mu = s.con_mu[c];
 #pragma unroll
   for (int k = 0; k < K; k++) out[k] = (isf || isl) ? sg1 * xs[k][col1] : a[k] + sg * mu * b[k];
 }
 // J row r dotted with x (LDS vector)
 template <int NC>
-__device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, const float* x) {
+__device__ __forceinline__ float row_dot(const Shared<NC>& s, int r, int nl, int ncon, const float* x) {
   const float* const xs[1] = {x};
   float o[1];
-  row_dotk<NC, 1>(s, r, xs, o);
+  row_dotk<NC, 1>(s, r, nl, ncon, xs, o);
   return o[0];
 }
 // J row r dotted with two LDS vectors in one pass
 template <int NC>
-__device__ __forceinline__ void row_dot2(const Shared<NC>& s, int r, const float* x, const float* y, float& rx,
-                                         float& ry) {
+__device__ __forceinline__ void row_dot2(const Shared<NC>& s, int r, int nl, int ncon, const float* x, const float* y,
+                                         float& rx, float& ry) {
   const float* const xs[2] = {x, y};
   float o[2];
-  row_dotk<NC, 2>(s, r, xs, o);
+  row_dotk<NC, 2>(s, r, nl, ncon, xs, o);
   rx = o[0];
   ry = o[1];
 }
@@ -966,7 +1016,7 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate) {
+__device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
   l = opaque_lane(l);
   // timing ablation only (-DPP3_AB_DUP=k, tools/ab_build.sh): phase k runs twice (the phases so
@@ -1137,7 +1187,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     const PairCon& q = *reinterpret_cast<const PairCon*>(&pc);
     const float mu = s.con_mu[c];
     const float dist = s.con_dist[c];
-    const float vel = row_dot(s, r, s.qvel);
+    const float vel = row_dot(s, r, nl, ncon, s.qvel);
     const float tran = q.tran;
     const float invw = (tran + mu * mu * tran) * 2.0f * mu * mu / m.impratio;
     const float imp = getimp(q.solimp, dist, q.margin);
@@ -1193,7 +1243,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       if (!valid[t]) continue;
       const int r = l + HW * t;
       float d1, d2;
-      row_dot2(s, r, s.qws, s.qacc_smooth, d1, d2);
+      row_dot2(s, r, nl, ncon, s.qws, s.qacc_smooth, d1, d2);
       const float x1 = d1 - ar[t];
       const float x2 = d2 - ar[t];
       xws[t] = x1;
@@ -1207,9 +1257,10 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
         csm += (x2 < 0) ? 0.5f * Dr[t] * x2 * x2 : 0.0f;
       }
     }
-    if (l < NV) {
-      ma_ws = mrow_dot(s, l, s.qws);
-      cws += 0.5f * (ma_ws - s.qfrc_smooth[l]) * (s.qws[l] - s.qacc_smooth[l]);
+    if (l < NV) {  // lane l: dof dn = pnat(l), the row it holds in mrow
+      const int dn = pnat(l);
+      ma_ws = mrow_dot_reg(mrow, s.qws);
+      cws += 0.5f * (ma_ws - s.qfrc_smooth[dn]) * (s.qws[dn] - s.qacc_smooth[dn]);
     }
     cws = hsum(cws, h);
     csm = hsum(csm, h);
@@ -1222,11 +1273,10 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   bool live = true;  // this env still iterating (per half)
   for (int iter = 0; iter < m.iterations; iter++) {
     // Ma, Jaref, constraint state/force
-    float ma = 0;
+    float ma = 0;  // (M qacc)[pnat(l)], kept in this lane's register through the line search
     if (l < NV) {
-      if (iter > 0 || use_smooth) ma = mrow_dot(s, l, s.qacc);
+      if (iter > 0 || use_smooth) ma = mrow_dot_reg(mrow, s.qacc);
       else ma = ma_ws;
-      s.Ma[l] = ma;
     }
     float jar[NR];
 #pragma unroll
@@ -1234,7 +1284,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       jar[t] = 0;
       if (!valid[t]) continue;
       const int r = l + HW * t;
-      const float x = iter > 0 ? row_dot(s, r, s.qacc) - ar[t] : (use_smooth ? xsm[t] : xws[t]);
+      const float x = iter > 0 ? row_dot(s, r, nl, ncon, s.qacc) - ar[t] : (use_smooth ? xsm[t] : xws[t]);
       jar[t] = x;
       float f, Dq = 0.0f;
       if (isfr[t]) {
@@ -1252,21 +1302,22 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     SYNC();
     // gradient, diagonal D per dof, contact Hessian blocks
     float gauss = 0;
-    if (l < NV) {
+    if (l < NV) {  // lane l: dof dn = pnat(l) (its (M qacc) entry is ma)
+      const int dn = pnat(l);
       float qc = 0;
-      if (l >= 6) qc += s.efc_force[l - 6];
-      float dD = (l >= 6) ? s.efc_D[l - 6] : 0.0f;
+      if (dn >= 6) qc += s.efc_force[dn - 6];
+      float dD = (dn >= 6) ? s.efc_D[dn - 6] : 0.0f;
       for (int i = 0; i < nl; i++)
-        if (s.lim_dof[i] == l) { qc += s.lim_sgn[i] * s.efc_force[NFR + i]; dD += s.efc_D[NFR + i]; }
+        if (s.lim_dof[i] == dn) { qc += s.lim_sgn[i] * s.efc_force[NFR + i]; dD += s.efc_D[NFR + i]; }
       for (int c = 0; c < ncon; c++) {
         const int r = NFR + nl + 4 * c;
         const float f0 = s.efc_force[r], f1 = s.efc_force[r + 1], f2 = s.efc_force[r + 2], f3 = s.efc_force[r + 3];
         const float mu = s.con_mu[c];
-        qc += s.Jc[c][0][l] * (f0 + f1 + f2 + f3) + mu * s.Jc[c][1][l] * (f0 - f1) + mu * s.Jc[c][2][l] * (f2 - f3);
+        qc += s.Jc[c][0][dn] * (f0 + f1 + f2 + f3) + mu * s.Jc[c][1][dn] * (f0 - f1) + mu * s.Jc[c][2][dn] * (f2 - f3);
       }
-      s.grad[l] = ma - s.qfrc_smooth[l] - qc;
-      s.dofD[l] = dD;
-      gauss = 0.5f * (ma - s.qfrc_smooth[l]) * (s.qacc[l] - s.qacc_smooth[l]);
+      s.grad[dn] = ma - s.qfrc_smooth[dn] - qc;
+      s.dofD[dn] = dD;
+      gauss = 0.5f * (ma - s.qfrc_smooth[dn]) * (s.qacc[dn] - s.qacc_smooth[dn]);
     }
     for (int c = l; c < ncon; c += HW) {
       const int r = NFR + nl + 4 * c;
@@ -1325,10 +1376,11 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     PHASE(7); l = opaque_lane(l);
     // line-search quadratics (Gauss part) and search-direction norm
     float q1 = 0, q2 = 0, sn = 0;
-    if (l < NV) {
-      const float sv = s.search[l];
-      const float mv = mrow_dot(s, l, s.search);
-      q1 = sv * (s.Ma[l] - s.qfrc_smooth[l]);
+    if (l < NV) {  // lane l: dof pnat(l)
+      const int dn = pnat(l);
+      const float sv = s.search[dn];
+      const float mv = mrow_dot_reg(mrow, s.search);
+      q1 = sv * (ma - s.qfrc_smooth[dn]);
       q2 = 0.5f * sv * mv;
       sn = sv * sv;
     }
@@ -1338,7 +1390,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     live = live && !(sn < MINVAL);
     float jv[NR];
 #pragma unroll
-    for (int t = 0; t < NR; t++) jv[t] = valid[t] ? row_dot(s, l + HW * t, s.search) : 0.0f;
+    for (int t = 0; t < NR; t++) jv[t] = valid[t] ? row_dot(s, l + HW * t, nl, ncon, s.search) : 0.0f;
     const float gtol = m.gtol_scale * sn;
     // Each row's cost on the line qacc + alpha*search is piecewise quadratic in alpha: the three
     // pieces' coefficients (below the lower switch point, above the upper one, in between) are
@@ -1457,7 +1509,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #ifdef PP3_PHASE_PROF
     {
       const int ew = wmax2(evals);
-      if (l == 0) { s.prof[20] += (uint64_t)evals; if (h == 0) s.prof[19] += (uint64_t)ew; }
+      PROF_ADD(19, ew);
+      PROF_ADD(20, evals);       // env 2b's evaluations (lane 20 is in the first half)
+      PROF_ADD(HW + 20, evals);  // env 2b+1's
     }
 #endif
     PHASE(8); l = opaque_lane(l);
@@ -1601,7 +1655,7 @@ __device__ __forceinline__ void sample_orientation(const DevModel& m, Key rng, f
 // gimu = [6][Li]), writes s.x.e.o[36]
 template <int NC>
 __device__ __forceinline__ void get_obs(Shared<NC>& s, const DevModel& m, float* gimu, int l, int h, float pose16, bool store,
-                                        const float* imu_stash = nullptr) {
+                                        const float* imu_stash PROF_PARAM) {
   const int part = m.partitionable;
   const Key rng{__float_as_uint(s.st[PP3_S_RNG]), __float_as_uint(s.st[PP3_S_RNG + 1])};
   const Key kl = split_i(rng, 6, l < 6 ? l : 0, part);  // lane i holds split(rng, 6)[i]
@@ -1811,8 +1865,8 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;
 #ifdef PP3_PHASE_PROF
-  if (l < NPROF) s.prof[l] = 0;
-  if (l == 0) s.prof_t = __builtin_amdgcn_s_memtime();
+  Prof pf_local{shader_cycles(), 0u};
+  Prof* pf = &pf_local;
 #endif
   // ---- every global load of this env step issued together (one memory round trip): state
   // record head, this lane's action-latency row and IMU row, the action, the obs history, the
@@ -1909,7 +1963,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    substep(s, *(const DevModel*)mp, l, h, true);
+    substep(s, *(const DevModel*)mp, l, h, true PROF_ARG);
   }
   SYNC();
 #ifdef PP3_AB_NO_EPILOGUE  // timing ablation only (tools/ab_build.sh): state out, no obs/reward
@@ -1926,7 +1980,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   const DevModel& m = *(const DevModel*)mq;
   const LaneRec<2> re = fetch_rec(m.lane_env, l);  // this lane's env constants (one round trip)
   // ---- observation (history already shifted in the prologue) ----
-  get_obs(s, m, gst + m.imu_off, l, h, re.f[LE_POSE16], own, imu_stash);
+  get_obs(s, m, gst + m.imu_off, l, h, re.f[LE_POSE16], own, imu_stash PROF_ARG);
   {
     if (own)
       for (int k = l; k < PP3_OBS_DIM; k += HW) oo[k] = s.x.e.o[k];
@@ -2103,7 +2157,8 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   PHASE(12);
   }
 #ifdef PP3_PHASE_PROF
-  if (l < NPROF) atomicAdd(&g_prof[l], (unsigned long long)s.prof[l]);
+  if (lane < NPROF) atomicAdd(&g_prof[lane], (unsigned long long)pf->acc);
+  if (lane == HW + 20) atomicAdd(&g_prof[20], (unsigned long long)pf->acc);
 #endif
 }
 
@@ -2164,7 +2219,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   if (l < NV) { s.qvel[l] = 0.0f; s.qws[l] = 0.0f; }
   if (l < NU) s.ctrl[l] = 0.0f;
   SYNC();
-  substep(s, m, l, h, false);  // pipeline_init: mjx.forward at (q, qd=0, ctrl=0)
+  substep(s, m, l, h, false PROF_NULL);  // pipeline_init: mjx.forward at (q, qd=0, ctrl=0)
   if (l < NQ) s.st[PP3_S_QPOS + l] = s.qpos[l];
   if (l < NV) { s.st[PP3_S_QVEL + l] = 0.0f; s.st[PP3_S_QACC_WS + l] = s.qws[l]; }
   if (l == 0) {
@@ -2176,7 +2231,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   if (own && l < m.Li) gst[m.imu_off + 5 * m.Li + l] = -1.0f;  // initial_imu_buffer gravity row
   __threadfence_block();
   __syncthreads();  // the gravity row above is global memory written by other lanes
-  get_obs(s, m, gst + m.imu_off, l, h, m.lane_env.g[LE_POSE16 / 4][l][LE_POSE16 % 4], own);
+  get_obs(s, m, gst + m.imu_off, l, h, m.lane_env.g[LE_POSE16 / 4][l][LE_POSE16 % 4], own, nullptr PROF_NULL);
   write_obs(s, m, nullptr, a.obs + (size_t)env * PP3_OBS_DIM * m.H, l, own);
   if (own && a.episode) {
     if (l < PP3_EP_STRIDE) a.episode[(size_t)env * PP3_EP_STRIDE + l] = 0.0f;
@@ -2223,7 +2278,7 @@ __global__ __launch_bounds__(WAVE, 2) void physics_kernel(PhysArgs a) {
   for (int i = 0; i < a.nsteps; i++) {
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    substep(s, *(const DevModel*)mp, l, h, true);
+    substep(s, *(const DevModel*)mp, l, h, true PROF_NULL);
   }
   if (!own) return;
   if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);

@@ -1,7 +1,8 @@
 """Diagnostic: per-phase shader-clock breakdown of env_step_kernel (PP3_PHASE_PROF build).
 
 PP3_LIB_PATH=pupperv3-mjx_amd/pupperv3_mjx/libpupper_hip_prof.so python tests/diag_phases.py
-Read the SHARES, not the absolute time (the stamps serialise the phases they bracket).
+Stamps are s_memtime reads into per-wave registers (a few % overhead; each stamp drains the LDS
+reads in flight).
 """
 import ctypes as C
 import os
@@ -27,7 +28,10 @@ def main():
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     steps = 20
     env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=False)
-    env.reset(make_keys(0, E))
+    st = env.reset(make_keys(0, E))
+    rec = st._record.copy()
+    rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]  # bench workload (configs[1])
+    env._put(_abi.F_STATE, rec)
     L = env._L
     acts = _lib.DeviceBuffer((steps + 5) * E * 48)
     _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, (steps + 5) * E * 12, 1, 0, -1.0, 1.0, None))

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--every", type=int, default=5)
+    ap.add_argument("--repeat", type=int, default=1,
+                    help="rollouts from the same reset, back to back (the later ones run on a warm GPU clock)")
     args = ap.parse_args()
     import numpy as np
     from bench import bench_kwargs
@@ -29,18 +31,27 @@ def main():
     st = env.reset(make_keys(0, E))
     rec = st._record.copy()
     rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]
-    env._put(_abi.F_STATE, rec)
+    obs0 = st.obs.copy()
     acts = _lib.DeviceBuffer(args.steps * E * 48, 0)
     _lib.check(env._L.pp3_fill_uniform(env._h, acts.ptr, args.steps * E * 12, 1234, 0, -1.0, 1.0, None))
     env.synchronize()
+    for rep in range(args.repeat):
+        env._put(_abi.F_STATE, rec)
+        env._put(_abi.F_OBS, obs0)
+        rollout(env, args, acts, E, rep)
+    env.close()
+
+
+def rollout(env, args, acts, E, rep):
+    import numpy as np
+    from pupperv3_mjx import _abi, _lib
     ms = C.c_float()
-    rows = []
     for i in range(args.steps):
         probe = i % args.every == 0
         if probe:
             _lib.check(env._L.pp3_set_pipeline_output(env._h, 1))
         _lib.check(env._L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + i * E * 48), 0, 1, C.byref(ms)))
-        r = {"step": i, "ms": round(ms.value, 5)}
+        r = {"rep": rep, "step": i, "ms": round(ms.value, 5)}
         if probe:
             p = env._get(_abi.F_PIPELINE)
             _lib.check(env._L.pp3_set_pipeline_output(env._h, 0))
@@ -53,9 +64,7 @@ def main():
             wave_dense = np.logical_or(selfc[0::2], selfc[1::2]) if E % 2 == 0 else selfc
             r.update(ncon_mean=round(float(ncon.mean()), 3), ncon_max=int(ncon.max()),
                      dense_waves=round(float(wave_dense.mean()), 4), z_mean=round(float(env._get(_abi.F_STATE)[:, 2].mean()), 4))
-        rows.append(r)
         print(json.dumps(r), flush=True)
-    env.close()
 
 
 if __name__ == "__main__":
