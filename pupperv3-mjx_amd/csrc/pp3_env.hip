@@ -354,10 +354,13 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
     } else {
       float ax[3], off[3], c[3];
       int b;
-      if (d < 6) {
+      if (d < 6) {  // column d - 3 of the base rotation (3-way selects, not a 9-way register index)
         float R[9];
         quat2mat(s.xquat[1], R);
-        ax[0] = R[d - 3]; ax[1] = R[3 + d - 3]; ax[2] = R[6 + d - 3];
+        const int cc = d - 3;
+        ax[0] = cc == 0 ? R[0] : (cc == 1 ? R[1] : R[2]);
+        ax[1] = cc == 0 ? R[3] : (cc == 1 ? R[4] : R[5]);
+        ax[2] = cc == 0 ? R[6] : (cc == 1 ? R[7] : R[8]);
         b = 1;
       } else {
         const int j = d - 5;
@@ -370,10 +373,13 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
     }
   }
   // composite inertia of the whole tree (body 1's subtree) for the 6 base dofs
+  {  // all ten sums first (independent DPP chains interleave), then the stores
+    float t[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) {
-    const float t = hsum(ci[k], h);
-    if (l == 0) s.crb_base[k] = t;
+    for (int k = 0; k < 10; k++) t[k] = hsum(ci[k], h);
+    if (l == 0)
+#pragma unroll
+      for (int k = 0; k < 10; k++) s.crb_base[k] = t[k];
   }
   // world positions of the robot collision spheres (lanes 0..7) and foot sites (16..19)
   const bool geom = l < m.nrobot_geom, foot = l >= 16 && l < 20;
@@ -623,11 +629,13 @@ __device__ __forceinline__ void rne_body_forces(Shared<NC>& s, int l, int h) {
     cross_force(f3, s.cvel[l], f2);
     for (int k = 0; k < 6; k++) { cf[k] = f1[k] + f3[k]; s.x.a.cacc[l][k] = cf[k]; }  // cfrc, in place
   }
+  // all six sums first (independent DPP chains interleave), then the stores
+  float t[6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const float t = hsum(cf[k], h);
-    if (l == 0) s.cfrc_base[k] = t;
-  }
+  for (int k = 0; k < 6; k++) t[k] = hsum(cf[k], h);
+  if (l == 0)
+#pragma unroll
+    for (int k = 0; k < 6; k++) s.cfrc_base[k] = t[k];
 }
 
 // composite inertia of body b's subtree times cdof d (for M), lanes < NV
@@ -1134,13 +1142,24 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   for (int it = l; it < ncon * NV; it += HW) {
     const int c = it / NV, i = it - c * NV;
     const uint32_t bit = 1u << i;
-    const float off[3] = {s.x.a.con_pos[c][0] - s.com[0], s.x.a.con_pos[c][1] - s.com[1], s.x.a.con_pos[c][2] - s.com[2]};
-    const float* cd = s.cdof[i];
+    // every operand loaded up front and pinned (one LDS round), then the three stores: otherwise
+    // each load is placed after the previous store (possible alias) and waited for on its own
+    float cp[3], cm[3], cd[6], fr[9];
+    uint32_t dm0 = s.con_dm[c][0], dm1 = s.con_dm[c][1];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { cp[k] = s.x.a.con_pos[c][k]; cm[k] = s.com[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; k++) cd[k] = s.cdof[i][k];
+#pragma unroll
+    for (int k = 0; k < 9; k++) fr[k] = s.x.a.con_frame[c][k];
+    PIN("+v"(cp[0]), "+v"(cp[1]), "+v"(cp[2]), "+v"(cm[0]), "+v"(cm[1]), "+v"(cm[2]), "+v"(cd[0]), "+v"(cd[1]),
+        "+v"(cd[2]), "+v"(cd[3]), "+v"(cd[4]), "+v"(cd[5]), "+v"(fr[0]), "+v"(fr[1]), "+v"(fr[2]), "+v"(fr[3]),
+        "+v"(fr[4]), "+v"(fr[5]), "+v"(fr[6]), "+v"(fr[7]), "+v"(fr[8]), "+v"(dm0), "+v"(dm1));
+    const float off[3] = {cp[0] - cm[0], cp[1] - cm[1], cp[2] - cm[2]};
     float cr[3], jp[3];
     cross3(cr, cd, off);
-    const float w = ((s.con_dm[c][1] & bit) ? 1.0f : 0.0f) - ((s.con_dm[c][0] & bit) ? 1.0f : 0.0f);
+    const float w = ((dm1 & bit) ? 1.0f : 0.0f) - ((dm0 & bit) ? 1.0f : 0.0f);
     for (int k = 0; k < 3; k++) jp[k] = w * (cd[3 + k] + cr[k]);
-    const float* fr = s.x.a.con_frame[c];
     s.Jc[c][0][i] = fr[0] * jp[0] + fr[1] * jp[1] + fr[2] * jp[2];
     s.Jc[c][1][i] = fr[3] * jp[0] + fr[4] * jp[1] + fr[5] * jp[2];
     s.Jc[c][2][i] = fr[6] * jp[0] + fr[7] * jp[1] + fr[8] * jp[2];
