@@ -591,10 +591,24 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
 }
 
 // RNE velocity/acceleration chain (mj_comVel + forward half of mj_rne): lanes 0..3 each
-// walk base -> leg l writing cvel and cacc of its links (lane 0 also the base).
+// walk base -> leg l writing cvel and cacc of its links (lane 0 also the base).  The leg's three
+// cdof rows and joint velocities are loaded (pinned) before the first store: a level's loads
+// would otherwise be placed after the previous level's stores and each waited for.
 template <int NC>
 __device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int l) {
   if (l >= 4) return;
+  float lcd[3][6], lqd[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int d = 6 + 3 * l + k;
+#pragma unroll
+    for (int c = 0; c < 6; c++) lcd[k][c] = s.cdof[d][c];
+    lqd[k] = s.qvel[d];
+  }
+  PIN("+v"(lcd[0][0]), "+v"(lcd[0][1]), "+v"(lcd[0][2]), "+v"(lcd[0][3]), "+v"(lcd[0][4]), "+v"(lcd[0][5]),
+      "+v"(lcd[1][0]), "+v"(lcd[1][1]), "+v"(lcd[1][2]), "+v"(lcd[1][3]), "+v"(lcd[1][4]), "+v"(lcd[1][5]),
+      "+v"(lcd[2][0]), "+v"(lcd[2][1]), "+v"(lcd[2][2]), "+v"(lcd[2][3]), "+v"(lcd[2][4]), "+v"(lcd[2][5]),
+      "+v"(lqd[0]), "+v"(lqd[1]), "+v"(lqd[2]));
   float cv[6] = {0, 0, 0, 0, 0, 0}, ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
   for (int d = 0; d < 3; d++)
     for (int k = 0; k < 6; k++) cv[k] += s.cdof[d][k] * s.qvel[d];
@@ -609,10 +623,10 @@ __device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int 
     for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv[k]; s.x.a.cacc[1][k] = ca[k]; }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const int b = 2 + 3 * l + k, d = 6 + 3 * l + k;
-    cross_motion(cdd, cv, s.cdof[d]);
-    const float qd = s.qvel[d];
-    for (int c = 0; c < 6; c++) { cv[c] += s.cdof[d][c] * qd; ca[c] += cdd[c] * qd; }
+    const int b = 2 + 3 * l + k;
+    cross_motion(cdd, cv, lcd[k]);
+    const float qd = lqd[k];
+    for (int c = 0; c < 6; c++) { cv[c] += lcd[k][c] * qd; ca[c] += cdd[c] * qd; }
     for (int c = 0; c < 6; c++) { s.cvel[b][c] = cv[c]; s.x.a.cacc[b][c] = ca[c]; }
   }
 }
@@ -638,25 +652,24 @@ __device__ __forceinline__ void rne_body_forces(Shared<NC>& s, int l, int h) {
     for (int k = 0; k < 6; k++) s.cfrc_base[k] = t[k];
 }
 
-// composite inertia of body b's subtree times cdof d (for M), lanes < NV
+// composite inertia of body b's subtree times cdof d (for M), lanes < NV.  Branch-free: the
+// base dofs read crb_base, a leg link its own cinert plus the (<= 2) links below it with weight 1
+// (weight 0 past the leg's end: adding exact zeros), so the loads form one block.
 template <int NC>
 __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m, int l) {
   if (l >= NV) return;
+  const bool base = l < 6;
+  const int b = base ? 2 : l - 4, last = 2 + 3 * ((b - 2) / 3) + 2;  // dof 6+3g+k <-> body 2+3g+k
+  const float* r0 = base ? s.crb_base : s.cinert[b];
   float crb[10];
-  if (l < 6) {
 #pragma unroll
-    for (int k = 0; k < 10; k++) crb[k] = s.crb_base[k];
-  } else {  // leg link: sum over the (<= 3) links below it in the same leg
-    const int b = l - 4, last = 2 + 3 * ((b - 2) / 3) + 2;  // dof 6+3g+k <-> body 2+3g+k
+  for (int k = 0; k < 10; k++) crb[k] = r0[k];
 #pragma unroll
-    for (int k = 0; k < 10; k++) crb[k] = s.cinert[b][k];
+  for (int o = 1; o < 3; o++) {
+    const int bb = b + o <= last ? b + o : b;
+    const float w = (!base && b + o <= last) ? 1.0f : 0.0f;
 #pragma unroll
-    for (int o = 1; o < 3; o++) {
-      const int bb = b + o <= last ? b + o : b;
-      const float w = b + o <= last ? 1.0f : 0.0f;
-#pragma unroll
-      for (int k = 0; k < 10; k++) crb[k] += w * s.cinert[bb][k];
-    }
+    for (int k = 0; k < 10; k++) crb[k] += w * s.cinert[bb][k];
   }
   mul_inert_vec(s.x.a.F[l], crb, s.cdof[l]);
 }
@@ -768,10 +781,16 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
       const int k = 3 * g + st;
       const float* c = col + 20 * g;
       float r[20];
+      // inner loops have constant trip counts (guards fold once g and st are unrolled): a bound
+      // that depends on an outer induction variable is not unrolled first and ends up as a
+      // runtime loop over s_set_gpr_idx register indexing
 #pragma unroll
-      for (int q = (k & ~3); q < 3 * g + 3; q += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(c + q);
-        r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+      for (int qq = 0; qq < 2; qq++) {
+        const int q = ((3 * g) & ~3) + 4 * qq;  // the float4 words holding this leg's 3 entries
+        if (q < 12 && q <= 3 * g + 2) {
+          const float4 v = *reinterpret_cast<const float4*>(c + q);
+          r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+        }
       }
 #pragma unroll
       for (int q = 12; q < 20; q += 4) {
@@ -782,7 +801,8 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
       dinv = (l == k) ? ik : dinv;
       const float lik = (l > k) ? a[k] * ik : 0.0f;  // zero on rows above the pivot and other legs
 #pragma unroll
-      for (int j = k + 1; j < 3 * g + 3; ++j) a[j] -= lik * r[j];
+      for (int jj = 0; jj < 3; ++jj)
+        if (jj > st) a[3 * g + jj] -= lik * r[3 * g + jj];
 #pragma unroll
       for (int j = 12; j < NV; ++j) a[j] -= lik * r[j];
       b -= lik * r[19];
