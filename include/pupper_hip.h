@@ -408,6 +408,10 @@ int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stri
 /* Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-clock totals of env_step_kernel
  * summed over envs (n <= 16 slots); returns PP3_ERR_ARG in the production build. */
 int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset);
+/* Diagnostic builds only: per-wave record of the last env-step launch, 8 words per wave (lifetime
+ * cycles, dense-Hessian substeps, max contacts, line-search evaluations, start and end stamps,
+ * HW_ID, XCC_ID). */
+int pp3_wave_profile(uint32_t* host_out, int32_t n);
 
 /* ---------------------------------------------------------------------------------------
  * On-device MLP policy in the reference's deployment format (export.py:13-81 convert_params:

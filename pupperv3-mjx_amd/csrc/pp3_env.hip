@@ -149,7 +149,11 @@ constexpr int NPROF = 22;  // 0..18 phase cycles, 19 line-search evaluations per
 __device__ unsigned long long g_prof[NPROF];
 struct Prof {
   uint32_t t, acc;
+  uint32_t t0, dense, ncmax, evals;  // per wave: start stamp, dense-Hessian substeps, max contacts, line-search evaluations
 };
+constexpr int MAXWAVE = 16384;
+__device__ uint32_t g_wave[MAXWAVE][8];  // last launch: lifetime cycles, dense substeps, max ncon, evaluations,
+                                         // start stamp, end stamp, HW_ID, XCC_ID
 __device__ __forceinline__ uint32_t shader_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
 #define PROF_PARAM , Prof* pf
 #define PROF_ARG , pf
@@ -1376,6 +1380,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     // coupling two legs (either env of the wave) switches the wave to the dense factorisation.
     AB_REP(10) {
       const bool dense = __ballot(lsup == 5) != 0;  // a leg-leg contact in either env
+#ifdef PP3_PHASE_PROF
+      if (pf) { pf->dense += dense ? 1u : 0u; pf->ncmax = pf->ncmax > (uint32_t)cmax ? pf->ncmax : (uint32_t)cmax; }
+#endif
       if (!dense) {
         const int lp = l < NV ? l : NV - 1, dn = pnat(lp);
         float a[NV];
@@ -1548,6 +1555,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #ifdef PP3_PHASE_PROF
     {
       const int ew = wmax2(evals);
+      if (pf) pf->evals += ew;
       PROF_ADD(19, ew);
       PROF_ADD(20, evals);       // env 2b's evaluations (lane 20 is in the first half)
       PROF_ADD(HW + 20, evals);  // env 2b+1's
@@ -1904,7 +1912,8 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;
 #ifdef PP3_PHASE_PROF
-  Prof pf_local{shader_cycles(), 0u};
+  const uint32_t t_start_ = shader_cycles();
+  Prof pf_local{t_start_, 0u, t_start_, 0u, 0u, 0u};
   Prof* pf = &pf_local;
 #endif
   // ---- every global load of this env step issued together (one memory round trip): state
@@ -1996,7 +2005,16 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   n_frames = PP3_AB_FRAMES;  // timing ablation only
 #endif
   asm volatile("" : "+s"(n_frames));  // one scalar load (an invariant load is otherwise re-issued per substep)
+  // VALU issue between the two waves of a SIMD goes by priority, then age: at equal priority the
+  // younger wave (wave slot 1 in 97 % of pairs) only gets the older one's leftover issue cycles
+  // and finished ~19 % later (per-wave lifetimes, diag_phases.py), and the launch ends with the
+  // slowest wave.  The two slots take turns at the higher priority, one substep each.
+  uint32_t hwid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  const int wslot = (int)(hwid & 1u);
   for (int f = 0; f < n_frames; f++) {
+    if (((f + wslot) & 1) != 0) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
     // opaque per iteration: keep model loads inside the substep (hoisting them costs more
     // registers than reloading them); the constant address space is restated after the asm so
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
@@ -2004,6 +2022,8 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     asm volatile("" : "+s"(mp));
     substep(s, *(const DevModel*)mp, l, h, true PROF_ARG);
   }
+  if (wslot) __builtin_amdgcn_s_setprio(1);  // the epilogue: the younger slot ahead
+  else __builtin_amdgcn_s_setprio(0);
   SYNC();
 #ifdef PP3_AB_NO_EPILOGUE  // timing ablation only (tools/ab_build.sh): state out, no obs/reward
   if (own)
@@ -2197,6 +2217,14 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   }
 #ifdef PP3_PHASE_PROF
   if (lane < NPROF) atomicAdd(&g_prof[lane], (unsigned long long)pf->acc);
+  if (lane == 0 && blockIdx.x < MAXWAVE) {
+    uint32_t hwid, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint32_t t_end = shader_cycles();
+    const uint32_t rec[8] = {t_end - pf->t0, pf->dense, pf->ncmax, pf->evals, pf->t0, t_end, hwid, xcc};
+    for (int k = 0; k < 8; k++) g_wave[blockIdx.x][k] = rec[k];
+  }
   if (lane == HW + 20) atomicAdd(&g_prof[20], (unsigned long long)pf->acc);
 #endif
 }
@@ -3134,6 +3162,20 @@ extern "C" int pp3_debug_read(float* out) {
   return PP3_OK;
 }
 #endif
+// prof build: per-wave record of the last env-step launch (lifetime cycles, dense substeps, max
+// contacts, line-search evaluations), n waves
+int pp3_wave_profile(uint32_t* host_out, int32_t n) {
+#ifdef PP3_PHASE_PROF
+  if (n > MAXWAVE) n = MAXWAVE;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wave), sizeof(uint32_t) * 8 * n));
+  return PP3_OK;
+#else
+  (void)host_out; (void)n;
+  return set_err(PP3_ERR_ARG, "pp3_wave_profile: library built without -DPP3_PHASE_PROF");
+#endif
+}
+
 int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset) {
 #ifdef PP3_PHASE_PROF
   if (n > NPROF) n = NPROF;

@@ -46,6 +46,30 @@ def main():
     print(f"E={E}: {ms.value / steps:.3f} ms/step (prof build); cycles per env-step per env: {tot / (E * steps):.0f}")
     for n, x in zip(NAMES, v):
         print(f"  {n:32s} {100 * x / tot:6.2f}%   {x / (E * steps):10.0f} cyc/env-step")
+    # per-wave record of the last launch: the kernel ends with its slowest wave
+    W = (E + 1) // 2
+    wv = (C.c_uint32 * (8 * W))()
+    _lib.check(L.pp3_wave_profile(wv, W))
+    w8 = np.array(wv[:], dtype=np.uint64).reshape(W, 8)
+    np.save(os.path.join(os.environ.get("PP3_DIAG_OUT", "/tmp"), "waves.npy"), w8)
+    w = w8[:, :4].astype(np.float64)
+    life = w[:, 0]
+    q = np.percentile(life, [50, 90, 99, 99.9])
+    print(f"  wave lifetime (last launch): mean {life.mean():.0f} p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} "
+          f"p99.9 {q[3]:.0f} max {life.max():.0f} cycles")
+    for name, col in (("dense substeps", 1), ("max contacts", 2), ("line-search evals", 3)):
+        v = w[:, col]
+        top = np.argsort(life)[-20:]
+        print(f"  {name:18s}: mean {v.mean():.2f} max {v.max():.0f} | slowest 20 waves mean {v[top].mean():.2f}")
+    # lifetime by dense / contacts
+    for d in range(int(w[:, 1].max()) + 1):
+        sel = w[:, 1] == d
+        if sel.any():
+            print(f"    dense={d}: {sel.sum():5d} waves, mean life {life[sel].mean():.0f}, max {life[sel].max():.0f}")
+    for c in range(int(w[:, 2].max()) + 1):
+        sel = w[:, 2] == c
+        if sel.any():
+            print(f"    ncmax={c}: {sel.sum():5d} waves, mean life {life[sel].mean():.0f}, max {life[sel].max():.0f}")
     nsub = steps * env.n_frames if hasattr(env, "n_frames") else steps * 5
     print(f"  line-search evaluations per substep: {buf[20] / (E * nsub):.2f} per env, "
           f"{buf[19] / (E / 2 * nsub):.2f} per wave (max of its two envs)")
