@@ -14,7 +14,7 @@ constexpr int NV = PP3_NV;
 constexpr int NQ = PP3_NQ;
 constexpr int NU = PP3_NU;
 constexpr int WAVE = 64;
-constexpr int NLMAX = 24;                 // joint-limit rows (12 joints x 2 sides)
+constexpr int NLMAX = 12;                 // joint-limit rows: one side per hinge at a time (checked at pp3_create)
 constexpr int NFR = 12;                   // frictionloss rows (hinge dofs)
 constexpr int MAX_ROBOT_GEOM = 16;        // DevModel table size for collidable geoms on moving bodies
 constexpr int NMPAIR_MAX = 128;           // nonzero (i, j<=i) entries of M

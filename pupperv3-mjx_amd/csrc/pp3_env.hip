@@ -1110,7 +1110,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     }
     const uint32_t mask = hballot(act, h);
     const int slot = __popc(mask & ((1u << l) - 1u));
-    if (act) {
+    if (act && slot < NLMAX) {  // (<= one side per hinge: never more than NLMAX rows)
       const int dof = 6 + j - 1;
       const float sg = (l & 1) ? -1.0f : 1.0f;  // J = -side
       s.lim_dof[slot] = dof;
@@ -1122,7 +1122,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       s.efc_D[r] = 1.0f / R;
       s.efc_aref[r] = -rl.f[LL_B] * (sg * s.qvel[dof]) - rl.f[LL_K] * imp * (value - rl.f[LL_MARGIN]);
     }
-    if (l == 0) s.nl = __popc(mask);
+    if (l == 0) s.nl = __popc(mask) < NLMAX ? __popc(mask) : NLMAX;
     if (l < NFR) {  // dof frictionloss rows (R, b precomputed: pos = 0)
       const int dof = 6 + l;
       s.efc_R[l] = rl.f[LL_FR_R];
@@ -2596,6 +2596,11 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
     clamp_solimp(mm->jnt_solimp[j], d->lim_solimp[j]);
     d->lim_margin[j] = (float)mm->jnt_margin[j];
     d->lim_invw[j] = (float)mm->dof_invweight0[mm->jnt_dofadr[j]];
+    // both sides of one hinge can only be violated together when the range is narrower than
+    // twice the margin; excluding that bounds the limit rows at one per hinge (NLMAX)
+    if (j > 0 && mm->jnt_limited[j] && !(mm->jnt_range[j][1] - mm->jnt_range[j][0] > 2.0 * mm->jnt_margin[j]))
+      return set_err(PP3_ERR_MODEL, "joint " + std::to_string(j) +
+                                        ": range narrower than twice the margin (both limit sides could be active)");
   }
   for (int i = 0; i < NQ; i++) { d->qpos0[i] = (float)mm->qpos0[i]; d->key_qpos[i] = (float)mm->key_qpos[i]; }
   for (int i = 0; i < NV; i++) {

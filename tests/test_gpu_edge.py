@@ -226,3 +226,14 @@ def test_results_independent_of_batch_layout(box_path):
             np.testing.assert_array_equal(s_full.done, np.concatenate([s_a.done, s_b.done]))
     finally:
         full.close(); a_part.close(); b_part.close()
+
+
+def test_create_rejects_two_sided_limit_margin(require_gpu):
+    """The kernel keeps at most one limit row per hinge (NLMAX = 12): a model whose joint range is
+    narrower than twice its margin (both sides could be violated at once) is rejected at create."""
+    import common
+    from pupperv3_mjx import _lib
+    m = common.pd_model().struct
+    m.jnt_margin[3] = 0.6 * (m.jnt_range[3][1] - m.jnt_range[3][0])
+    with pytest.raises(_lib.PupperHipError, match="twice the margin"):
+        G.env_with_model(common.MODEL_XML, m, 2)
