@@ -54,6 +54,20 @@ def main():
         if stats:
             shutil.copy(stats[0], dst + "_kernel_stats.csv")
         json.dump(out, open(dst + "_pmc_summary.json", "w"), indent=1)
+        # the bench's roofline.traffic / valu_issue source, keyed to the kernel sources it was measured on
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import bench
+        if "hbm_bytes_per_launch" in out and "per_wave" in out:
+            json.dump({"source": dst + "_pmc_summary.json (tools/gpu_profile.sh on MI355X, bench.py --steps 50 --warmup 5 "
+                                     "--no-latency-floor --no-extras)",
+                       "src_sha16": bench.kernel_source_sha16(), "envs": 4096, "dr": False,
+                       "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
+                       "fetch_bytes_per_launch": out["fetch_bytes_per_launch"],
+                       "write_bytes_per_launch": out["write_bytes_per_launch"],
+                       "valu_insts_per_wave": out["per_wave"]["SQ_INSTS_VALU"], "envs_per_wave": 2,
+                       "waves": out.get("waves"), "kernel_avg_ns": out.get("kernel_avg_ns")},
+                      open(os.path.join(root, "profiles", "traffic_current.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
