@@ -1379,7 +1379,11 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
     // touch one leg (+ base) keep H arrowhead -> tree-sparse LDL in permuted order; a contact
     // coupling two legs (either env of the wave) switches the wave to the dense factorisation.
     AB_REP(10) {
+#ifdef PP3_AB_NO_DENSE  // timing ablation only: the arrowhead solve even with leg-leg contacts (wrong physics)
+      const bool dense = false;
+#else
       const bool dense = __ballot(lsup == 5) != 0;  // a leg-leg contact in either env
+#endif
 #ifdef PP3_PHASE_PROF
       if (pf) { pf->dense += dense ? 1u : 0u; pf->ncmax = pf->ncmax > (uint32_t)cmax ? pf->ncmax : (uint32_t)cmax; }
 #endif
