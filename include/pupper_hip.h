@@ -360,7 +360,7 @@ int32_t pp3_terrain_slots(const pp3_env_t* env);
  * the substep parity tests; writes the pipeline record of the last substep. */
 int pp3_physics_step(pp3_env_t* env, const float* ctrl_dev, int32_t nsteps, void* stream);
 
-/* Auto-reset mode = brax.envs.training.wrap(env, episode_length, action_repeat=1) on device
+/* Auto-reset mode = brax.envs.training.wrap(env, episode_length, action_repeat) on device
  * ([ext] brax 0.12.1 EpisodeWrapper + AutoResetWrapper, the wrappers Brax PPO puts around
  * PupperV3Env).  Per env: episode step counter, truncation flag and the
  * episode sum_reward / length; pp3_reset stores the reset's qpos/qvel/qacc_warmstart and obs
@@ -378,6 +378,13 @@ int pp3_physics_step(pp3_env_t* env, const float* ctrl_dev, int32_t nsteps, void
 #define PP3_EP_STRIDE 4
 #define PP3_FIRST_STRIDE 55
 int pp3_set_auto_reset(pp3_env_t* env, int32_t episode_length);
+/* brax.envs.training.wrap(..., action_repeat=k) (EpisodeWrapper.step scans env.step k times with
+ * the same action): in auto-reset mode every pp3_step launches the env step k times; reward =
+ * the sum over the k repeats, the episode counter and length advance by k, and done, truncation
+ * and the auto-reset are decided after the last repeat (the env's own done of that repeat, as in
+ * Brax).  k = 1 is the plain mode; k > 1 needs auto-reset mode (PP3_ERR_ARG otherwise); turning
+ * auto-reset off resets k to 1. */
+int pp3_set_action_repeat(pp3_env_t* env, int32_t action_repeat);
 
 /* Device pointer + element count per env of a field (PP3_F_*). */
 int pp3_field(pp3_env_t* env, int32_t field, void** dev_ptr, int64_t* elems_per_env);

@@ -72,6 +72,7 @@ struct alignas(16) Shared {
   float fric, kp, kd;
   int dr_on;
   float ep[PP3_EP_STRIDE], ep_prev_done;  // auto-reset mode: episode record, previous done
+  float ep_racc;                          // action repeat: the reward summed over this step's earlier repeats
   // kinematics / dynamics of the current substep (the last one feeds the epilogue)
   float xpos[NB][3], xquat[NB][4], xaxis[NJ][3];
   float com[4];
@@ -1899,6 +1900,7 @@ struct StepArgs {
   const float* first_state;  // [N][PP3_FIRST_STRIDE]
   const float* first_obs;    // [N][36H]
   int episode_length;
+  int repeat, phase;  // auto-reset mode: action_repeat and this launch's repeat index
   int N;
 };
 
@@ -1952,7 +1954,10 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++) v[t] = l + HW * t < PP3_S_ACT_BUF ? gst[l + HW * t] : 0.0f;
   // auto-reset mode: the previous step's done and this env's episode record (kept in LDS)
   if (a.episode) {
-    if (l == 0) s.ep_prev_done = a.done[env];
+    if (l == 0) {
+      s.ep_prev_done = a.done[env];  // the previous wrapper step's (earlier repeats leave it alone)
+      s.ep_racc = a.phase > 0 ? a.reward[env] : 0.0f;
+    }
     if (l < PP3_EP_STRIDE) s.ep[l] = a.episode[(size_t)env * PP3_EP_STRIDE + l];
   }
   load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
@@ -2170,21 +2175,29 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   const bool resample = stepc > m.resample_step;
   const float reward = fminf(fmaxf(rsum * m.dt, 0.0f), 10000.0f);
   bool done_out = isdone;
-  if (a.episode) {  // brax EpisodeWrapper.step / AutoResetWrapper.step ([ext] brax 0.12.1)
-    const float keep = 1.0f - s.ep_prev_done;            // previous step done -> counters restart
-    const float ep_rec = l < PP3_EP_STRIDE ? s.ep[l] : 0.0f;
-    const float steps = s.ep[PP3_EP_STEPS] * keep + 1.0f;
-    const bool trunc_hit = steps >= (float)a.episode_length;
-    done_out = isdone || trunc_hit;
-    float v = steps;
-    if (l == PP3_EP_TRUNCATION) v = (trunc_hit && !isdone) ? 1.0f : 0.0f;
-    if (l == PP3_EP_SUM_REWARD) v = (ep_rec + reward) * keep;
-    if (l == PP3_EP_LENGTH) v = (ep_rec + 1.0f) * keep;
-    if (own && l < PP3_EP_STRIDE) a.episode[(size_t)env * PP3_EP_STRIDE + l] = v;
+  // brax EpisodeWrapper.step / AutoResetWrapper.step ([ext] brax 0.12.1): with action_repeat k a
+  // wrapper step is k launches with the same action; the reward is summed over them, and the
+  // episode bookkeeping, done and the auto-reset happen at the last one
+  const bool last = a.phase == a.repeat - 1;
+  float rout = reward;
+  if (a.episode) {
+    rout = reward + s.ep_racc;
+    if (last) {
+      const float keep = 1.0f - s.ep_prev_done;  // previous step done -> counters restart
+      const float ep_rec = l < PP3_EP_STRIDE ? s.ep[l] : 0.0f;
+      const float steps = s.ep[PP3_EP_STEPS] * keep + (float)a.repeat;
+      const bool trunc_hit = steps >= (float)a.episode_length;
+      done_out = isdone || trunc_hit;
+      float v = steps;
+      if (l == PP3_EP_TRUNCATION) v = (trunc_hit && !isdone) ? 1.0f : 0.0f;
+      if (l == PP3_EP_SUM_REWARD) v = (ep_rec + rout) * keep;
+      if (l == PP3_EP_LENGTH) v = (ep_rec + (float)a.repeat) * keep;
+      if (own && l < PP3_EP_STRIDE) a.episode[(size_t)env * PP3_EP_STRIDE + l] = v;
+    }
   }
   if (own && l == 0) {
-    a.reward[env] = reward;
-    a.done[env] = done_out ? 1.0f : 0.0f;
+    a.reward[env] = rout;
+    if (!a.episode || last) a.done[env] = done_out ? 1.0f : 0.0f;
     a.metrics[(size_t)env * PP3_NMETRIC] =
         sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
   }
@@ -2204,7 +2217,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (isdone || resample) stepc = 0;
   if (l == 0) s.st[PP3_S_STEP] = (float)stepc;
   if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
-  if (a.episode && done_out) {  // AutoResetWrapper: pipeline state and obs <- the reset's
+  if (a.episode && last && done_out) {  // AutoResetWrapper: pipeline state and obs <- the reset's
     const float* fs = a.first_state + (size_t)env * PP3_FIRST_STRIDE;
     for (int i = l; i < PP3_FIRST_STRIDE; i += HW) s.st[PP3_S_QPOS + i] = fs[i];
     const float* fo = a.first_obs + (size_t)env * PP3_OBS_DIM * m.H;
@@ -2395,6 +2408,7 @@ struct pp3_env {
   float* first_state;
   float* first_obs;
   int episode_length;
+  int action_repeat;  // auto-reset mode: launches per wrapper step (1 otherwise)
   float* terrain;  // TerrainRec rows (pp3_set_terrain), null until first set
   int nbox;        // world box-geom slots in the model
   hipEvent_t ev0, ev1;
@@ -2874,6 +2888,7 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   if (rc) return rc;
   HIPCHK(hipSetDevice(device));
   pp3_env* e = new pp3_env();
+  e->action_repeat = 1;
   memset(e, 0, sizeof(*e));
   e->device = device;
   e->N = num_envs;
@@ -2973,9 +2988,12 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   a.first_obs = e->first_obs;
   a.episode_length = e->episode_length;
   a.N = e->N;
-  if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
-  else hipLaunchKernelGGL(env_step_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
-  HIPCHK(hipGetLastError());
+  a.repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;
+  for (a.phase = 0; a.phase < a.repeat; a.phase++) {  // action_repeat: the same action, k launches
+    if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
+    else hipLaunchKernelGGL(env_step_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
+    HIPCHK(hipGetLastError());
+  }
   return PP3_OK;
 }
 
@@ -2996,6 +3014,16 @@ int pp3_set_auto_reset(pp3_env_t* e, int32_t episode_length) {
                           hipMemcpyDeviceToDevice, e->stream));
   }
   e->episode_length = episode_length > 0 ? episode_length : 0;
+  if (e->episode_length == 0) e->action_repeat = 1;
+  return PP3_OK;
+}
+
+int pp3_set_action_repeat(pp3_env_t* e, int32_t action_repeat) {
+  if (!e) return set_err(PP3_ERR_ARG, "null env");
+  if (action_repeat < 1) return set_err(PP3_ERR_ARG, "action_repeat must be >= 1");
+  if (action_repeat > 1 && e->episode_length <= 0)
+    return set_err(PP3_ERR_ARG, "action_repeat > 1 needs auto-reset mode (pp3_set_auto_reset first)");
+  e->action_repeat = action_repeat;
   return PP3_OK;
 }
 

@@ -59,6 +59,7 @@ def load() -> C.CDLL:
     L.pp3_phase_profile.argtypes = [C.POINTER(C.c_uint64), i32, i32]
     L.pp3_wave_profile.argtypes = [C.POINTER(C.c_uint32), i32]
     L.pp3_set_auto_reset.argtypes = [vp, i32]
+    L.pp3_set_action_repeat.argtypes = [vp, i32]
     L.pp3_policy_create.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(vp)]
     L.pp3_policy_act.argtypes = [vp, vp, i64, i32, vp, i64, vp]
     L.pp3_policy_out_dim.argtypes = [vp]
@@ -85,7 +86,7 @@ def load() -> C.CDLL:
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
                  "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
                  "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
-                 "pp3_wave_profile", "pp3_set_auto_reset", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy",
+                 "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy",
                  "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
                  "pp3_comm_allreduce", "pp3_comm_barrier"):
         getattr(L, name).restype = C.c_int
@@ -114,7 +115,7 @@ EXPORTED_SYMBOLS = (
     "pp3_num_envs", "pp3_state_stride", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
     "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
-    "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset",
+    "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
     "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
     "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_comm_rank", "pp3_comm_world",

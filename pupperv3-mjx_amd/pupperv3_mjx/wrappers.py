@@ -15,8 +15,13 @@ step kernel (pp3_set_auto_reset), so a rollout never leaves the GPU:
     (the state its last reset produced) where done.  The env's own info (rng, command, last
     action, latency buffers, ...) carries over, as in Brax.
 
+  * action_repeat k (EpisodeWrapper.step's lax.scan over env.step with the same action): every
+    step() is k launches of the env step; reward = the sum over the k repeats, info['steps'] and
+    the episode length advance by k, and done / truncation / the auto-reset follow the last
+    repeat (pp3_set_action_repeat).
+
 Domain randomisation (the DomainRandomizationVmapWrapper role) is PupperV3Env.
-set_domain_randomization.  action_repeat > 1 is not supported (the reference trains with 1).
+set_domain_randomization.
 """
 from __future__ import annotations
 
@@ -30,13 +35,15 @@ class AutoResetEpisodeEnv:
     """EpisodeWrapper + AutoResetWrapper semantics over a batched PupperV3Env."""
 
     def __init__(self, env: PupperV3Env, episode_length: int = 1000, action_repeat: int = 1):
-        if action_repeat != 1:
-            raise NotImplementedError("action_repeat != 1 is not supported on device")
         if episode_length <= 0:
             raise ValueError("episode_length must be positive")
+        if action_repeat < 1:
+            raise ValueError("action_repeat must be >= 1")
         self.env = env
         self.episode_length = int(episode_length)
+        self.action_repeat = int(action_repeat)
         _lib.check(env._L.pp3_set_auto_reset(env._h, self.episode_length))
+        _lib.check(env._L.pp3_set_action_repeat(env._h, self.action_repeat))
 
     # brax Env surface
     @property

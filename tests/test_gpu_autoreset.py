@@ -83,3 +83,78 @@ def test_auto_reset_episode_semantics(require_gpu, tmp_path, episode_length, ter
             assert n_trunc > 0
     finally:
         e.close()
+
+
+def _oracle_repeat_step(oe, rec, obs, action, ep, prev_done, first_state, first_obs, L, k):
+    """brax EpisodeWrapper.step with action_repeat k (lax.scan of env.step, rewards summed), then
+    AutoResetWrapper: counters restart after a done step, the last repeat's env done decides."""
+    keep = 1.0 - prev_done
+    st = dict(state=G.record_to_oracle_state(rec), obs=obs.astype(np.float64))
+    rsum, flagged = 0.0, False
+    for _ in range(k):
+        o = oe.step(st, action.astype(np.float64))
+        st = dict(state=o["state"], obs=o["obs"])
+        rsum += o["reward"]
+        flagged = flagged or o["boundary"] > 0
+    steps = ep[_abi.EP_STEPS] * keep + k
+    hit = steps >= L
+    done = bool(o["done"]) or hit
+    trunc = 1.0 if (hit and not o["done"]) else 0.0
+    out_obs = o["obs"].astype(np.float32)
+    if done:
+        out_obs = first_obs.copy()
+    ep_new = np.array([steps, trunc, (ep[_abi.EP_SUM_REWARD] + rsum) * keep, (ep[_abi.EP_LENGTH] + k) * keep])
+    return out_obs, float(done), ep_new, rsum, dict(o, boundary=1 if flagged else 0)
+
+
+def test_action_repeat(require_gpu, tmp_path):
+    """wrap(env, episode_length=8, action_repeat=3): every step() is 3 env steps with the same
+    action; reward = their sum, counters advance by 3 (a truncation at step 9), done and the
+    auto-reset follow the last repeat -- against the restated wrapper over the oracle."""
+    path = common.write_model(tmp_path, 0)
+    n, k, L = 8, 3, 8
+    e = PupperV3Env(**common.fixture_kwargs(path, terminal_body_z=0.1), num_envs=n)
+    try:
+        env = wrappers.wrap(e, episode_length=L, action_repeat=k)
+        st = env.reset(make_keys(4, n))
+        first_state = e._get(_abi.F_FIRST_STATE)
+        first_obs = e._get(_abi.F_FIRST_OBS)
+        oe = O.OracleEnv(e.sys_model.struct, e.config_struct, precision="f32")
+        rs = np.random.RandomState(6)
+        fb = G.FlipBudget()
+        n_trunc = 0
+        for t in range(6):
+            a = rs.uniform(-1, 1, size=(n, 12)).astype(np.float32)
+            prev = st
+            ep_prev = e._get(_abi.F_EPISODE)
+            st = env.step(prev, a)
+            ep = e._get(_abi.F_EPISODE)
+            for i in range(n):
+                oobs, odone, oep, rsum, o = _oracle_repeat_step(
+                    oe, prev._record[i], prev.obs[i], a[i], ep_prev[i], float(prev.done[i]), first_state[i],
+                    first_obs[i], L, k)
+                ok = st.done[i] == odone and abs(st.reward[i] - rsum) <= 3e-3
+                if odone:
+                    ok = ok and np.array_equal(st._record[i, 0:_abi.FIRST_STRIDE], first_state[i])
+                    ok = ok and np.array_equal(st.obs[i], first_obs[i])
+                else:
+                    ok = ok and np.abs(st.obs[i] - oobs).max() <= 5e-3
+                fb.check(ok, o, f"step {t} env {i}")
+                np.testing.assert_array_equal(ep[i, _abi.EP_STEPS], oep[0])
+                if st.done[i] == odone:
+                    np.testing.assert_array_equal(ep[i, _abi.EP_TRUNCATION], oep[1])
+                n_trunc += int(ep[i, _abi.EP_TRUNCATION])
+        fb.finish()
+        assert n_trunc > 0  # 3 + 3 + 3 = 9 >= 8 steps
+    finally:
+        e.close()
+
+
+def test_action_repeat_needs_auto_reset(require_gpu):
+    from pupperv3_mjx import _lib
+    e = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=2)
+    try:
+        with pytest.raises(_lib.PupperHipError, match="auto-reset"):
+            _lib.check(e._L.pp3_set_action_repeat(e._h, 2))
+    finally:
+        e.close()
