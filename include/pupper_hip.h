@@ -415,6 +415,25 @@ int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stri
 /* Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-clock totals of env_step_kernel
  * summed over envs (n <= 16 slots); returns PP3_ERR_ARG in the production build. */
 int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset);
+/* Rendering (environment.py:545-547 PupperV3Env.render -> Brax PipelineEnv.render, the policy
+ * videos of utils.py:214-293; not on the training path).  A z-buffer rasteriser over a triangle
+ * soup built on the host by pupperv3_mjx/render.py from the model's visual geoms:
+ *   tris [ntri][9]        vertices in the geom's local frame (device)
+ *   tri_geom [ntri]       geom index of each triangle (device)
+ *   geom_rgb [ngeom][3]   colour in 0..1 (device)
+ *   geom_xf [F][ngeom][12] per frame: world rotation (row-major 3x3) then translation (device)
+ *   cams [F][16]          per frame: position, right, up, forward (unit), focal length in pixels
+ *                         (= height / 2 / tan(fovy / 2)), 3 pad (device)
+ *   scene [17]            floor checker colours rgb1[3], rgb2[3], square size, floor height, sky
+ *                         top[3], sky bottom[3], ambient, diffuse, floor on (HOST pointer)
+ *   out [F][H][W][3]      u8 RGB (device)
+ * Nearest fragment per pixel by a 64-bit atomicMin of (depth bits, rgb): deterministic.
+ * Synchronous on `stream` (NULL = default stream); its own errors via pp3_render_last_error(). */
+int pp3_render(int32_t device, const float* tris, const int32_t* tri_geom, int32_t ntri, const float* geom_rgb,
+               int32_t ngeom, const float* geom_xf, const float* cams, int32_t nframes, int32_t height,
+               int32_t width, const float* scene, uint8_t* out, void* stream);
+const char* pp3_render_last_error(void);
+
 /* Diagnostic builds only: per-wave record of the last env-step launch, 8 words per wave (lifetime
  * cycles, dense-Hessian substeps, max contacts, line-search evaluations, start and end stamps,
  * HW_ID, XCC_ID). */

@@ -273,6 +273,27 @@ class PupperV3Env:
     def sys(self) -> domain_randomization.System:
         return self._sys
 
+    def render(self, trajectory, camera: Optional[str] = None, height: int = 240, width: int = 320,
+               env_index: int = 0, meshdir: Optional[str] = None) -> List[np.ndarray]:
+        """environment.py:545-547 (-> Brax PipelineEnv.render): one u8 [height, width, 3] frame per
+        state of `trajectory` (States, PipelineStates or qpos arrays; batched ones give env
+        `env_index`), rasterised on the GPU by render.py / pp3_render.  `camera` defaults to "track"
+        as in the reference (the stock model defines only "tracking_cam"; an unknown name raises,
+        as MuJoCo does); None after that default is not possible, -1 selects a free camera."""
+        from . import render as _render
+        camera = camera or "track"
+        qs = []
+        for st in trajectory:
+            ps = getattr(st, "pipeline_state", st)
+            q = np.asarray(getattr(ps, "q", ps), dtype=np.float64)
+            qs.append(q[env_index] if q.ndim == 2 else q)
+        key = meshdir
+        if getattr(self, "_render_scene", None) is None or self._render_key != key:
+            self._render_scene = _render.Scene(self.sys_model, meshdir)
+            self._render_key = key
+        cam = None if camera == -1 else camera
+        return _render.render_qpos(self._render_scene, qs, cam, height, width, self.device)
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._L.pp3_destroy(self._h)

@@ -24,6 +24,7 @@ from __future__ import annotations
 import copy
 import ctypes
 import math
+import os
 import xml.etree.ElementTree as ET
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple, Union
@@ -150,6 +151,8 @@ class CompiledModel:
     geom_friction: np.ndarray
     jnt_range: np.ndarray
     xml: str
+    # rendering-only description (render.py): visual geoms, mesh assets, materials, cameras
+    visual: Dict = field(default_factory=dict)
 
     # --- name -> id helpers (mujoco.mj_name2id equivalents, environment.py:17-29) ---
     def body_id(self, name: str) -> int:
@@ -200,6 +203,9 @@ def load(path_or_xml: Union[str, "ET.ElementTree"], is_string: bool = False) -> 
         with open(path_or_xml) as f:
             xml = f.read()
         root = ET.fromstring(xml)
+        cm = _compile(root, xml)
+        cm.visual["source_dir"] = os.path.dirname(os.path.abspath(path_or_xml))
+        return cm
     return _compile(root, xml)
 
 
@@ -245,7 +251,9 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
                 friction=_vec(a["friction"], 3, [1, 0.005, 0.0001]), solmix=float(a["solmix"]),
                 solref=_vec(a["solref"], 2, [0.02, 1]),
                 solimp=_vec(a["solimp"], 5, [0.9, 0.95, 0.001, 0.5, 2]),
-                margin=float(a["margin"]), gap=float(a["gap"])))
+                margin=float(a["margin"]), gap=float(a["gap"]),
+                group=int(a.get("group", "0")), mesh=a.get("mesh"), material=a.get("material"),
+                rgba=_vec(a.get("rgba", "0.5 0.5 0.5 1"), 4)))
             bodies[bid].geoms.append(len(geoms) - 1)
         for s in node.findall("site"):
             a = defaults.resolve("site", s.get("class", cls), _SITE_DEFAULTS)
@@ -583,6 +591,7 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
 
     body_geomadr = np.array([b.geoms[0] if b.geoms else -1 for b in bodies])
     body_geomnum = np.array([len(b.geoms) for b in bodies])
+    visual = _visual(root, geoms, [b.name for b in bodies], angle_deg)
     return CompiledModel(
         struct=m,
         body_names=[b.name for b in bodies],
@@ -598,7 +607,41 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
         geom_friction=np.array([g["friction"] for g in geoms]),
         jnt_range=np.array([joints[j]["range"] for j in range(len(joints))]),
         xml=xml,
+        visual=visual,
     )
+
+
+def _visual(root: ET.Element, geoms: List[dict], body_names: List[str], angle_deg: bool) -> Dict:
+    """What render.py needs: every geom's shape/pose/group/colour, the mesh assets (file, scale),
+    materials and textures (rgba / builtin checker and gradient colours), the cameras."""
+    compiler = root.find("compiler")
+    vis: Dict = {"meshdir": compiler.get("meshdir", "") if compiler is not None else "",
+                 "meshes": {}, "materials": {}, "textures": {}, "cameras": {}, "skybox": None}
+    for asset in root.findall("asset"):
+        for m in asset.findall("mesh"):
+            name = m.get("name") or os.path.splitext(os.path.basename(m.get("file", "")))[0]
+            vis["meshes"][name] = dict(file=m.get("file"), scale=_vec(m.get("scale", "1 1 1"), 3))
+        for t in asset.findall("texture"):
+            tex = dict(type=t.get("type", "cube"), builtin=t.get("builtin", "none"),
+                       rgb1=_vec(t.get("rgb1", "0.8 0.8 0.8"), 3), rgb2=_vec(t.get("rgb2", "0.5 0.5 0.5"), 3))
+            if tex["type"] == "skybox":
+                vis["skybox"] = tex
+            if t.get("name"):
+                vis["textures"][t.get("name")] = tex
+        for mt in asset.findall("material"):
+            vis["materials"][mt.get("name")] = dict(
+                rgba=_vec(mt.get("rgba", "1 1 1 1"), 4), texture=mt.get("texture"),
+                texrepeat=_vec(mt.get("texrepeat", "1 1"), 2), texuniform=mt.get("texuniform", "false") == "true")
+    vis["geoms"] = [dict(type=g["type"], size=g["size"], pos=g["pos"], quat=g["quat"], body=g["body"],
+                         group=g["group"], mesh=g["mesh"], material=g["material"], rgba=g["rgba"], name=g["name"])
+                    for g in geoms]
+    wb = root.find("worldbody")
+    for c in wb.iter("camera"):
+        vis["cameras"][c.get("name", f"camera{len(vis['cameras'])}")] = dict(
+            mode=c.get("mode", "fixed"), target=body_names.index(c.get("target")) if c.get("target") in body_names else -1,
+            pos=_vec(c.get("pos", "0 0 0"), 3), quat=_orientation(c.attrib, angle_deg),
+            fovy=float(c.get("fovy", "45")), parent_world=c in list(wb))
+    return vis
 
 
 # ----------------------------------------------------------------------------------
