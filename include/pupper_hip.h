@@ -434,9 +434,10 @@ int pp3_render(int32_t device, const float* tris, const int32_t* tri_geom, int32
                int32_t width, const float* scene, uint8_t* out, void* stream);
 const char* pp3_render_last_error(void);
 
-/* Diagnostic builds only: per-wave record of the last env-step launch, 8 words per wave (lifetime
+/* Diagnostic builds only: per-wave record of the last env-step launch, 288 words per wave (lifetime
  * cycles, dense-Hessian substeps, max contacts, line-search evaluations, start and end stamps,
- * HW_ID, XCC_ID). */
+ * HW_ID, XCC_ID, then 19 per-phase cycle counts, contacts summed over substeps, substeps that
+ * used the second constraint-row slot, s_memrealtime (100 MHz) at start and end, 1 unused; then 128 phase stamps and their 128 phase ids). */
 int pp3_wave_profile(uint32_t* host_out, int32_t n);
 
 /* ---------------------------------------------------------------------------------------

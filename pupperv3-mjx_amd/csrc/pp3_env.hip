@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "pp3_device.h"
@@ -147,14 +148,22 @@ __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 // end of the launch (gfx950 has no SHADER_CYCLES hwreg).
 #ifdef PP3_PHASE_PROF
 constexpr int NPROF = 22;  // 0..18 phase cycles, 19 line-search evaluations per wave (max of its two envs), 20 per env
-__device__ unsigned long long g_prof[NPROF];
 struct Prof {
   uint32_t t, acc;
   uint32_t t0, dense, ncmax, evals;  // per wave: start stamp, dense-Hessian substeps, max contacts, line-search evaluations
+  uint32_t csum, slot2;               // contacts summed over substeps (max of the two envs), substeps using row slot 1
+  uint32_t n, tr0, tr1, k0, k1;       // stamp trace: stamp i held by lane i % 64 in tr{i / 64}, its phase in k{i / 64}
 };
 constexpr int MAXWAVE = 16384;
-__device__ uint32_t g_wave[MAXWAVE][8];  // last launch: lifetime cycles, dense substeps, max ncon, evaluations,
-                                         // start stamp, end stamp, HW_ID, XCC_ID
+constexpr int NTRACE = 128;
+constexpr int WREC = 32 + 2 * NTRACE;  // + the stamp trace (stamps, then phase ids; 0xffffffff = unused)
+__device__ uint32_t g_wave[MAXWAVE][WREC];  // last launch: lifetime cycles, dense substeps, max ncon, evaluations,
+                                            // start stamp, end stamp, HW_ID, XCC_ID, 8..26 the wave's cycles
+                                            // per phase, 27 csum, 28 slot2, 29/30 s_memrealtime at start/end
+// per-wave slots summed on the host: no contended device-scope atomics at wave exit (45 k atomics
+// on 22 addresses clogged the memory path that the remaining waves' scalar loads share, and
+// stalled them by 20-80 k cycles: tools/wave_trace.py)
+__device__ unsigned long long g_prof[MAXWAVE][NPROF];
 __device__ __forceinline__ uint32_t shader_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
 #define PROF_PARAM , Prof* pf
 #define PROF_ARG , pf
@@ -167,6 +176,11 @@ __device__ __forceinline__ uint32_t shader_cycles() { return (uint32_t)__builtin
       const uint32_t t_ = shader_cycles();                                  \
       pf->acc += ((int)(threadIdx.x) == (k)) ? (t_ - pf->t) : 0u;         \
       pf->t = t_;                                                           \
+      const uint32_t i_ = pf->n++;                                          \
+      if ((i_ & 63u) == (threadIdx.x & 63u)) {                              \
+        if (i_ < 64u) { pf->tr0 = t_; pf->k0 = (k); }                        \
+        else if (i_ < 128u) { pf->tr1 = t_; pf->k1 = (k); }                  \
+      }                                                                     \
     }                                                                       \
   } while (0)
 #else
@@ -1386,7 +1400,11 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       const bool dense = __ballot(lsup == 5) != 0;  // a leg-leg contact in either env
 #endif
 #ifdef PP3_PHASE_PROF
-      if (pf) { pf->dense += dense ? 1u : 0u; pf->ncmax = pf->ncmax > (uint32_t)cmax ? pf->ncmax : (uint32_t)cmax; }
+      if (pf) {
+        pf->dense += dense ? 1u : 0u;
+        pf->ncmax = pf->ncmax > (uint32_t)cmax ? pf->ncmax : (uint32_t)cmax;
+        pf->csum += (uint32_t)cmax;
+      }
 #endif
       if (!dense) {
         const int lp = l < NV ? l : NV - 1, dn = pnat(lp);
@@ -1466,6 +1484,9 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
       chi[t][1] = fr ? fl[t] * jw : 0.0f;
       rowany[t] = __ballot(valid[t]) != 0;  // wave-uniform: skip row slots no lane uses
     }
+#ifdef PP3_PHASE_PROF
+    if (pf && NR > 1 && rowany[NR - 1]) pf->slot2++;
+#endif
     // cost and derivatives of the 1-D piecewise quadratic at alpha (alpha is per half)
     auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
       float t0 = 0, t1 = 0, t2 = 0;
@@ -1919,7 +1940,8 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   float* gst = a.state + (size_t)env * stride;
 #ifdef PP3_PHASE_PROF
   const uint32_t t_start_ = shader_cycles();
-  Prof pf_local{t_start_, 0u, t_start_, 0u, 0u, 0u};
+  const uint32_t rt_start_ = (uint32_t)__builtin_amdgcn_s_memrealtime();  // 100 MHz, chip-wide
+  Prof pf_local{t_start_, 0u, t_start_, 0u, 0u, 0u, 0u, 0u, 0u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   Prof* pf = &pf_local;
 #endif
   // ---- every global load of this env step issued together (one memory round trip): state
@@ -2233,7 +2255,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   PHASE(12);
   }
 #ifdef PP3_PHASE_PROF
-  if (lane < NPROF) atomicAdd(&g_prof[lane], (unsigned long long)pf->acc);
+  if (lane < NPROF - 1 && blockIdx.x < MAXWAVE) g_prof[blockIdx.x][lane] += pf->acc;
   if (lane == 0 && blockIdx.x < MAXWAVE) {
     uint32_t hwid, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
@@ -2241,8 +2263,19 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     const uint32_t t_end = shader_cycles();
     const uint32_t rec[8] = {t_end - pf->t0, pf->dense, pf->ncmax, pf->evals, pf->t0, t_end, hwid, xcc};
     for (int k = 0; k < 8; k++) g_wave[blockIdx.x][k] = rec[k];
+    g_wave[blockIdx.x][27] = pf->csum;
+    g_wave[blockIdx.x][28] = pf->slot2;
+    g_wave[blockIdx.x][29] = rt_start_;
+    g_wave[blockIdx.x][30] = (uint32_t)__builtin_amdgcn_s_memrealtime();
   }
-  if (lane == HW + 20) atomicAdd(&g_prof[20], (unsigned long long)pf->acc);
+  if (lane < 19 && blockIdx.x < MAXWAVE) g_wave[blockIdx.x][8 + lane] = pf->acc;
+  if (blockIdx.x < MAXWAVE) {
+    g_wave[blockIdx.x][32 + lane] = pf->tr0;
+    g_wave[blockIdx.x][32 + 64 + lane] = pf->tr1;
+    g_wave[blockIdx.x][32 + NTRACE + lane] = pf->k0;
+    g_wave[blockIdx.x][32 + NTRACE + 64 + lane] = pf->k1;
+  }
+  if (lane == HW + 20 && blockIdx.x < MAXWAVE) g_prof[blockIdx.x][NPROF - 1] += pf->acc;
 #endif
 }
 
@@ -3199,13 +3232,13 @@ extern "C" int pp3_debug_read(float* out) {
   return PP3_OK;
 }
 #endif
-// prof build: per-wave record of the last env-step launch (lifetime cycles, dense substeps, max
-// contacts, line-search evaluations), n waves
+// prof build: per-wave record of the last env-step launch (WREC words per wave: lifetime cycles,
+// dense substeps, max contacts, line-search evaluations, ..., cycles per phase, stamp trace), n waves
 int pp3_wave_profile(uint32_t* host_out, int32_t n) {
 #ifdef PP3_PHASE_PROF
   if (n > MAXWAVE) n = MAXWAVE;
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wave), sizeof(uint32_t) * 8 * n));
+  HIPCHK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wave), sizeof(uint32_t) * WREC * n));
   return PP3_OK;
 #else
   (void)host_out; (void)n;
@@ -3217,10 +3250,17 @@ int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset) {
 #ifdef PP3_PHASE_PROF
   if (n > NPROF) n = NPROF;
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_prof), sizeof(uint64_t) * n));
+  std::vector<unsigned long long> all((size_t)MAXWAVE * NPROF);
+  HIPCHK(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(g_prof), sizeof(unsigned long long) * all.size()));
+  unsigned long long sum[NPROF] = {0};
+  for (int w = 0; w < MAXWAVE; w++)
+    for (int k = 0; k < NPROF; k++) sum[k] += all[(size_t)w * NPROF + k];
+  sum[20] += sum[NPROF - 1];  // the second env's evaluations (lane HW + 20)
+  sum[NPROF - 1] = 0;
+  for (int k = 0; k < n; k++) host_out[k] = sum[k];
   if (reset) {
-    unsigned long long z[NPROF] = {0};
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+    std::fill(all.begin(), all.end(), 0ull);
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), all.data(), sizeof(unsigned long long) * all.size()));
   }
   return PP3_OK;
 #else

@@ -48,9 +48,9 @@ def main():
         print(f"  {n:32s} {100 * x / tot:6.2f}%   {x / (E * steps):10.0f} cyc/env-step")
     # per-wave record of the last launch: the kernel ends with its slowest wave
     W = (E + 1) // 2
-    wv = (C.c_uint32 * (8 * W))()
+    wv = (C.c_uint32 * (288 * W))()
     _lib.check(L.pp3_wave_profile(wv, W))
-    w8 = np.array(wv[:], dtype=np.uint64).reshape(W, 8)
+    w8 = np.array(wv[:], dtype=np.uint64).reshape(W, 288)
     np.save(os.path.join(os.environ.get("PP3_DIAG_OUT", "/tmp"), "waves.npy"), w8)
     w = w8[:, :4].astype(np.float64)
     life = w[:, 0]
@@ -70,6 +70,20 @@ def main():
         sel = w[:, 2] == c
         if sel.any():
             print(f"    ncmax={c}: {sel.sum():5d} waves, mean life {life[sel].mean():.0f}, max {life[sel].max():.0f}")
+    # which phases grow with contacts: per-wave phase cycles regressed on contact-substeps
+    ph = w8[:, 8:27].astype(np.float64)
+    cs = w8[:, 27].astype(np.float64)
+    s2 = w8[:, 28].astype(np.float64)
+    print(f"  contact-substeps per wave: mean {cs.mean():.1f}; substeps with row slot 1: mean {s2.mean():.2f}")
+    A = np.stack([np.ones_like(cs), cs, s2, w[:, 1], w[:, 3]], 1)
+    coef_l = np.linalg.lstsq(A, life, rcond=None)[0]
+    print(f"  lifetime ~ {coef_l[0]:.0f} + {coef_l[1]:.0f}*csum + {coef_l[2]:.0f}*slot2 + {coef_l[3]:.0f}*dense "
+          f"+ {coef_l[4]:.0f}*evals")
+    print(f"  {'phase':32s} {'mean':>8s} {'/csum':>7s} {'/slot2':>7s} {'/dense':>7s} {'/eval':>7s} {'slow20':>8s}")
+    top = np.argsort(life)[-20:]
+    for k, n in enumerate(NAMES):
+        c = np.linalg.lstsq(A, ph[:, k], rcond=None)[0]
+        print(f"  {n:32s} {ph[:, k].mean():8.0f} {c[1]:7.0f} {c[2]:7.0f} {c[3]:7.0f} {c[4]:7.0f} {ph[top, k].mean():8.0f}")
     nsub = steps * env.n_frames if hasattr(env, "n_frames") else steps * 5
     print(f"  line-search evaluations per substep: {buf[20] / (E * nsub):.2f} per env, "
           f"{buf[19] / (E / 2 * nsub):.2f} per wave (max of its two envs)")
