@@ -157,6 +157,7 @@ struct DevModel {
   float pair_margin[PP3_MAX_PAIR];
   float pair_tran[PP3_MAX_PAIR];       // body_invweight0 translational sum
   int32_t pair_sup[PP3_MAX_PAIR];      // Jacobian column support: leg 0..3 (+base), 4 base only, 5 dense
+                                       // (leg-leg: | 8 | lower leg << 4 | higher leg << 6)
   uint32_t pair_dm[PP3_MAX_PAIR][2];   // dof masks (ancestor-or-self) of the pair's two bodies
   PairTab pair_rec;                    // PairRec of pair p, word-group major; sphere-box: s2 = -1 - (box slot)
   PairCon pair_con[PP3_MAX_PAIR];

@@ -889,6 +889,142 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
   return x;
 }
 
+// ldl_arrow_solve with leg `lb` (per half) moved into the base block.  A Hessian whose leg-leg
+// couplings (contacts between two legs) all involve leg lb is arrowhead once lb's three rows are
+// counted with the base: eliminating the other three legs (the same three rounds) creates fill
+// only in their own rows, lb's rows and the base, and the 9 x 9 Schur complement of [leg lb |
+// base] is factored and solved in registers on every lane, instead of the dense path's 18
+// sequential pivots and 34 broadcast substitution steps.  Lane p holds permuted row p in a[];
+// lb's columns are carried in e[] (the array's lb entries are zeroed, so the per-lane sums over
+// the other legs' columns stay exact).
+__device__ __forceinline__ float ldl_arrow_solve_b(float (&a)[NV], float rhs, int l, float* col /* >= 93 floats */,
+                                                   int lb) {
+  l = opaque_lane(l);
+  const int slot = l < NV ? l : NV;
+  const int lp = l < NV ? l : NV - 1;
+  const bool brow = lp >= 3 * lb && lp < 3 * lb + 3;  // one of leg lb's rows
+  float e[3];
+#pragma unroll
+  for (int jj = 0; jj < 3; jj++) e[jj] = lb == 0 ? a[jj] : lb == 1 ? a[3 + jj] : lb == 2 ? a[6 + jj] : a[9 + jj];
+#pragma unroll
+  for (int g = 0; g < 4; g++)
+#pragma unroll
+    for (int jj = 0; jj < 3; jj++) a[3 * g + jj] = (lb == g) ? 0.0f : a[3 * g + jj];
+  float dinv = 1.0f;
+#pragma unroll
+  for (int st = 0; st < 3; st++) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      col[20 * g + slot] = a[3 * g + st];
+      if (l == 3 * g + st) col[20 * g + 19] = rhs;  // pivot rhs
+    }
+    SYNC();
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const int k = 3 * g + st;
+      const float* c = col + 20 * g;
+      float r[20], rb[3];
+#pragma unroll
+      for (int qq = 0; qq < 2; qq++) {
+        const int q = ((3 * g) & ~3) + 4 * qq;
+        if (q < 12 && q <= 3 * g + 2) {
+          const float4 v = *reinterpret_cast<const float4*>(c + q);
+          r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+        }
+      }
+#pragma unroll
+      for (int q = 12; q < 20; q += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(c + q);
+        r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
+      }
+#pragma unroll
+      for (int jj = 0; jj < 3; jj++) rb[jj] = c[3 * lb + jj];  // pivot row's entries in lb's columns (symmetry)
+      const bool act = lb != g;  // lb's rows are not pivots here
+      const float ik = frcp(fmaxf(r[k], MINVAL));
+      dinv = (l == k && act) ? ik : dinv;
+      // rows after the pivot, and lb's rows (eliminated with the base); other legs' entries are 0
+      const float lik = (act && (l > k || brow)) ? a[k] * ik : 0.0f;
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj)
+        if (jj > st) a[3 * g + jj] -= lik * r[3 * g + jj];
+#pragma unroll
+      for (int j = 12; j < NV; ++j) a[j] -= lik * r[j];
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) e[jj] -= lik * rb[jj];
+      rhs -= lik * r[19];
+    }
+    SYNC();
+  }
+  // Schur complement of [lb | base] (rows lb0..2, base0..5) and its rhs: ONE exchange
+  const int bi = brow ? lp - 3 * lb : (lp >= 12 ? 3 + lp - 12 : -1);
+  if (l < NV && bi >= 0) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) col[9 * bi + c] = e[c];
+#pragma unroll
+    for (int c = 0; c < 6; c++) col[9 * bi + 3 + c] = a[12 + c];
+    col[84 + bi] = rhs;
+  }
+  SYNC();
+  float S[9][9], y[9];
+#pragma unroll
+  for (int q = 0; q < 84; q += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(col + q);
+    const float w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (q + u < 81) S[(q + u) / 9][(q + u) % 9] = w4[u];
+  }
+  {
+    const float4 v0 = *reinterpret_cast<const float4*>(col + 84);
+    const float4 v1 = *reinterpret_cast<const float4*>(col + 88);
+    y[0] = v0.x; y[1] = v0.y; y[2] = v0.z; y[3] = v0.w;
+    y[4] = v1.x; y[5] = v1.y; y[6] = v1.z; y[7] = v1.w;
+    y[8] = col[92];
+  }
+  SYNC();  // col is rewritten by the next use
+  float db[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const float ik = frcp(fmaxf(S[k][k], MINVAL));
+    db[k] = ik;
+#pragma unroll
+    for (int i = 8; i > k; --i) {  // descending: rows below still hold their unscaled column k
+      const float lik = S[i][k] * ik;
+#pragma unroll
+      for (int j = k + 1; j <= i; ++j) S[i][j] -= lik * S[j][k];
+      S[i][k] = lik;
+    }
+  }
+#pragma unroll
+  for (int c = 1; c < 9; c++)
+#pragma unroll
+    for (int k = 0; k < c; k++) y[c] = y[c] - S[c][k] * y[k];
+#pragma unroll
+  for (int c = 0; c < 9; c++) y[c] = y[c] * db[c];
+#pragma unroll
+  for (int c = 7; c >= 0; --c)
+#pragma unroll
+    for (int i = 8; i > c; --i) y[c] = y[c] - S[i][c] * y[i];
+  // the other legs' rows: U x = y from registers (lb and base parts) and the rows below in the
+  // same leg (DPP), as in ldl_arrow_solve
+  const int li = lp < 12 ? lp - 3 * (lp / 3) : 3;
+  float t = rhs;
+#pragma unroll
+  for (int c = 0; c < 3; c++) t -= e[c] * y[c];
+#pragma unroll
+  for (int c = 0; c < 6; c++) t -= a[12 + c] * y[3 + c];
+  const float u1 = a[1] + a[4] + a[7] + a[10], u2 = a[2] + a[5] + a[8] + a[11];
+  float x = t * dinv;
+  float v1 = dpp_shl1(x);
+  x = (li == 1) ? (t - u2 * v1) * dinv : x;
+  v1 = dpp_shl1(x);
+  const float v2 = dpp_shl2(x);
+  x = (li == 0) ? (t - u1 * v1 - u2 * v2) * dinv : x;
+#pragma unroll
+  for (int c = 0; c < 9; c++) x = (bi == c) ? y[c] : x;
+  return x;
+}
+
 // a[npos(j)] += w . J[.][j] over natural columns [J0, J1) (arrowhead Hessian rows)
 template <int J0, int J1>
 __device__ __forceinline__ void hess_acc_p(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
@@ -940,7 +1076,7 @@ __device__ __forceinline__ void row_dotk(const Shared<NC>& s, int r, int nl, int
   float a[K], b[K];
 #pragma unroll
   for (int k = 0; k < K; k++) { a[k] = 0.0f; b[k] = 0.0f; }
-  if (__ballot(isc && sup == 5)) {
+  if (__ballot(isc && (sup & 7) == 5)) {
 #pragma unroll
     for (int i = 0; i < NV; i++) {
       const float j0 = s.Jc[c][0][i], jt = s.Jc[c][t][i];
@@ -1029,13 +1165,69 @@ __device__ __forceinline__ int choice_from_uniform(const GFloat* dist, int n, fl
   return li < n ? li : n - 1;
 }
 
-// Newton direction with a leg-leg contact (dense Hessian, rare): out of line, so its registers
-// and code do not shape the allocation and scheduling of the arrowhead path
+// Newton direction with a leg-leg contact (rare): out of line, so its registers and code do not
+// shape the allocation and scheduling of the arrowhead path.  When every leg-leg contact of an
+// env involves one leg lb (the usual case: one pair of legs touching), the Hessian is arrowhead
+// with lb counted in the base block (ldl_arrow_solve_b); otherwise the dense LDL^T below.
 template <int NC>
 using LdsShared = __attribute__((address_space(3))) Shared<NC>;
 template <int NC>
-__device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l, int h, int cmax, int ncon) {
+__device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l, int h, int cmax, int ncon, int lsup) {
   Shared<NC>& s = *(Shared<NC>*)sp;
+  {
+    // per half: the leg common to all of its leg-leg contacts (sup = 5 | 8 | lo << 4 | hi << 6)
+    const bool ll = (lsup & 7) == 5;
+    const bool known = (lsup & 8) != 0;
+    const int p = (lsup >> 4) & 3, q = (lsup >> 6) & 3;
+    const uint64_t bll = __ballot(ll), bunk = __ballot(ll && !known);
+    uint64_t bl[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) bl[g] = __ballot(ll && known && (p == g || q == g));
+    int lbh[2];
+    bool okh[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+      const uint64_t hm = hh ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+      const int n = __popcll(bll & hm);
+      int b = 0;
+      bool found = false;
+#pragma unroll
+      for (int g = 3; g >= 0; g--)
+        if (__popcll(bl[g] & hm) == n) { b = g; found = true; }
+      okh[hh] = found && (bunk & hm) == 0;
+      lbh[hh] = b;
+    }
+    if (okh[0] && okh[1]) {
+      const int lb = h ? lbh[1] : lbh[0];
+      const int lp = l < NV ? l : NV - 1, dn = pnat(lp);  // permuted row held by this lane
+      float a[NV];
+#pragma unroll
+      for (int j = 0; j < NV; j++) a[j] = s.M[dn][pnat(j)];
+      const float dD = s.dofD[dn];
+#pragma unroll
+      for (int j = 0; j < NV; j++) a[j] += (j == lp) ? dD : 0.0f;
+      for (int c = 0; c < cmax; c++) {
+        const int sa = __builtin_amdgcn_readlane(lsup, c), sb = __builtin_amdgcn_readlane(lsup, HW + c);
+        if (c < ncon) {
+          const float* G = s.con_G[c];
+          const float jn = s.Jc[c][0][dn], j1 = s.Jc[c][1][dn], j2 = s.Jc[c][2][dn];
+          const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
+          const float w1 = jn * G[1] + j1 * G[3];
+          const float w2 = jn * G[2] + j2 * G[4];
+          // a leg-leg contact: every leg block (the legs it does not touch have zero columns)
+          const bool any = (sa & 7) == 5 || (sb & 7) == 5;
+          hess_acc_p<0, 6>(a, s.Jc[c], w0, w1, w2);
+          if (any || sa == 0 || sb == 0) hess_acc_p<6, 9>(a, s.Jc[c], w0, w1, w2);
+          if (any || sa == 1 || sb == 1) hess_acc_p<9, 12>(a, s.Jc[c], w0, w1, w2);
+          if (any || sa == 2 || sb == 2) hess_acc_p<12, 15>(a, s.Jc[c], w0, w1, w2);
+          if (any || sa == 3 || sb == 3) hess_acc_p<15, 18>(a, s.Jc[c], w0, w1, w2);
+        }
+      }
+      const float x = ldl_arrow_solve_b(a, s.grad[dn], l, &s.x.L[0][0], lb);
+      if (l < NV) s.search[dn] = -x;
+      return;
+    }
+  }
   const int li = l < NV ? l : NV - 1;
   float a[NV], dinv = 1.0f;
 #pragma unroll
@@ -1397,7 +1589,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #ifdef PP3_AB_NO_DENSE  // timing ablation only: the arrowhead solve even with leg-leg contacts (wrong physics)
       const bool dense = false;
 #else
-      const bool dense = __ballot(lsup == 5) != 0;  // a leg-leg contact in either env
+      const bool dense = __ballot((lsup & 7) == 5) != 0;  // a leg-leg contact in either env
 #endif
 #ifdef PP3_PHASE_PROF
       if (pf) {
@@ -1438,7 +1630,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #endif
         if (l < NV) s.search[dn] = -x;
       } else {
-        dense_search<NC>((LdsShared<NC>*)&s, l, h, cmax, ncon);
+        dense_search<NC>((LdsShared<NC>*)&s, l, h, cmax, ncon, lsup);
       }
     }
     SYNC();
@@ -2746,8 +2938,8 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
       else if (c1 == c2) sup = c1;
       else if (c1 == 4) sup = c2;
       else if (c2 == 4) sup = c1;
-      else sup = 5;
-      d->pair_sup[p] = sup < 0 ? 5 : sup;
+      else sup = 5 | 8 | ((c1 < c2 ? c1 : c2) << 4) | ((c1 < c2 ? c2 : c1) << 6);  // leg-leg: the pair
+      d->pair_sup[p] = sup < 0 ? 5 : sup;  // (5 without bit 3: legs unknown -> dense LDL^T)
     }
     d->pair_dm[p][0] = d->body_dofmask[mm->cgeom_bodyid[g1]];
     d->pair_dm[p][1] = d->body_dofmask[mm->cgeom_bodyid[g2]];

@@ -118,13 +118,21 @@ def states_on_boxes(model, n, seed=0, z_range=(0.15, 0.175)):
     return qpos, qvel, qws, ctrl
 
 
-def states_with_self_contact(model, jnt_range, n, seed=0, z=0.5):
+def _leg_of_body(b):
+    return -1 if b == 0 else (4 if b == 1 else (b - 2) // 3)
+
+
+def states_with_self_contact(model, jnt_range, n, seed=0, z=0.5, kind="any"):
     """Seeded states (joint angles uniform in their ranges, base at height z) in which at least
     one contact is between two robot geoms (a sphere-sphere pair of two different legs), found
     by rejection sampling against the oracle.  These contacts couple two legs in the Jacobian,
-    which takes the kernel's dense (non-arrowhead) Hessian factorisation path."""
+    which takes the kernel's leg-leg Newton path (dense_search).  kind="disjoint": the contacts
+    couple two disjoint pairs of legs (no leg common to all), which the kernel can only factor
+    densely; "any": at least one leg-leg contact (one pair: the arrowhead solve with that pair's
+    leg in the base block)."""
     from oracle import oracle as O
     static = {int(model.cgeom_id[g]) for g in range(model.ncgeom) if model.cgeom_bodyid[g] == 0}
+    body = {int(model.cgeom_id[g]): int(model.cgeom_bodyid[g]) for g in range(model.ncgeom)}
     rs = np.random.RandomState(seed)
     lo, hi = jnt_range[1:, 0], jnt_range[1:, 1]
     qs = []
@@ -135,7 +143,16 @@ def states_with_self_contact(model, jnt_range, n, seed=0, z=0.5):
         p = O.mj_step(model, q, np.zeros(18), np.zeros(18), q[7:].copy(), nsteps=1)[3]
         k = int(p[_abi.P_NCON])
         g = p[_abi.P_CON_GEOM:_abi.P_CON_GEOM + 2 * k].reshape(k, 2).astype(int)
-        if any(a not in static and b not in static for a, b in g):
+        if kind == "any":
+            if any(a not in static and b not in static for a, b in g):
+                qs.append(q)
+            continue
+        pairs = set()
+        for a, b in g:
+            la, lb = _leg_of_body(body[a]), _leg_of_body(body[b])
+            if 0 <= la < 4 and 0 <= lb < 4 and la != lb:
+                pairs.add((min(la, lb), max(la, lb)))
+        if len(pairs) > 1 and not any(all(x in pr for pr in pairs) for x in range(4)):
             qs.append(q)
     qpos = np.array(qs)
     qvel = rs.normal(scale=0.3, size=(n, 18))
