@@ -1255,7 +1255,7 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate PROF_PARAM) {
+__device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
   l = opaque_lane(l);
   // timing ablation only (-DPP3_AB_DUP=k, tools/ab_build.sh): phase k runs twice (the phases so
@@ -1520,6 +1520,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   SYNC();
   PHASE(5); l = opaque_lane(l);
   const int cmax = wmax2(ncon);
+  int weight = cmax;  // returned: the wave's load this substep (contacts, +2 on the leg-leg path)
   bool live = true;  // this env still iterating (per half)
   for (int iter = 0; iter < m.iterations; iter++) {
     // Ma, Jaref, constraint state/force
@@ -1591,6 +1592,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
 #else
       const bool dense = __ballot((lsup & 7) == 5) != 0;  // a leg-leg contact in either env
 #endif
+      weight = cmax + (dense ? 2 : 0);
 #ifdef PP3_PHASE_PROF
       if (pf) {
         pf->dense += dense ? 1u : 0u;
@@ -1798,7 +1800,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   // the next substep rebuilds its rows)
   if (l < NV) s.efc_aref[l] = s.qvel[l];
   SYNC();
-  if (!integrate) return;
+  if (!integrate) return weight;
   // ---- phase 8: Euler (eulerdamp disabled) ----
   const float hstep = m.h;
   float vn = 0;
@@ -1821,6 +1823,7 @@ __device__ __forceinline__ void substep(Shared<NC>& s, const DevModel& m, int l,
   }
   SYNC();
   PHASE(9);
+  return weight;
 }
 
 // ------------------------------------------------------------------------------------
@@ -2235,17 +2238,31 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   uint32_t hwid;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
   const int wslot = (int)(hwid & 1u);
+  int heavy = 0;  // the previous substep's load was high (1) / very high (2): this wave sets the launch's tail
   for (int f = 0; f < n_frames; f++) {
-    if (((f + wslot) & 1) != 0) __builtin_amdgcn_s_setprio(1);
+    // the heavy waves (many contacts, leg-leg Newton path) ahead of their partners, which have
+    // slack; between equals the two slots alternate
+    const int prio = heavy == 2 ? 3 : 2 * heavy + ((f + wslot) & 1);
+    if (prio == 3) __builtin_amdgcn_s_setprio(3);
+    else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (prio == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     // opaque per iteration: keep model loads inside the substep (hoisting them costs more
     // registers than reloading them); the constant address space is restated after the asm so
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    substep(s, *(const DevModel*)mp, l, h, true PROF_ARG);
+    const int wgt = substep(s, *(const DevModel*)mp, l, h, true PROF_ARG);
+#ifndef PP3_HEAVY
+#define PP3_HEAVY 5
+#endif
+#ifndef PP3_HEAVY2
+#define PP3_HEAVY2 100
+#endif
+    heavy = wgt >= PP3_HEAVY2 ? 2 : (wgt >= PP3_HEAVY ? 1 : 0);
   }
-  if (wslot) __builtin_amdgcn_s_setprio(1);  // the epilogue: the younger slot ahead
+  if (heavy) __builtin_amdgcn_s_setprio(3);  // the epilogue: heavy waves, then the younger slot, ahead
+  else if (wslot) __builtin_amdgcn_s_setprio(1);
   else __builtin_amdgcn_s_setprio(0);
   SYNC();
 #ifdef PP3_AB_NO_EPILOGUE  // timing ablation only (tools/ab_build.sh): state out, no obs/reward
