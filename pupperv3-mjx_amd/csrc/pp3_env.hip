@@ -193,6 +193,15 @@ __device__ __forceinline__ uint32_t shader_cycles() { return (uint32_t)__builtin
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+// wave priority by load (env_step_kernel): contact-weight thresholds (contacts of the busier env
+// of the wave, +2 on the leg-leg Newton path) for the upper priority pair / the top priority
+#ifndef PP3_HEAVY
+#define PP3_HEAVY 5
+#endif
+#ifndef PP3_HEAVY2
+#define PP3_HEAVY2 100
+#endif
+
 #ifdef PP3_DEBUG
 __device__ float g_dbg[512];  // last Newton iteration of env 0 (debug build only)
 #endif
@@ -2253,12 +2262,6 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
     const int wgt = substep(s, *(const DevModel*)mp, l, h, true PROF_ARG);
-#ifndef PP3_HEAVY
-#define PP3_HEAVY 5
-#endif
-#ifndef PP3_HEAVY2
-#define PP3_HEAVY2 100
-#endif
     heavy = wgt >= PP3_HEAVY2 ? 2 : (wgt >= PP3_HEAVY ? 1 : 0);
   }
   if (heavy) __builtin_amdgcn_s_setprio(3);  // the epilogue: heavy waves, then the younger slot, ahead
