@@ -316,6 +316,12 @@ __device__ __forceinline__ void b_rotate(float r[3], const float v[3], const flo
 }
 
 // MuJoCo impedance (getimpedance), solimp pre-clamped on the host
+// solimp with a power other than 1 or 2: out of line -- its four powf calls are ~750 instructions
+// per call site that the common powers never run, inside a substep loop whose code is about the
+// size of the CU pair's instruction cache
+__device__ __attribute__((noinline)) float getimp_pow(float x, float mid, float p) {
+  return (x <= mid) ? powf(x, p) / powf(mid, p - 1.0f) : 1.0f - powf(1.0f - x, p) / powf(1.0f - mid, p - 1.0f);
+}
 __device__ __forceinline__ float getimp(const float* si, float pos, float margin) {
   float x = fabsf((pos - margin) / si[2]);
   if (x >= 1.0f) return si[1];
@@ -326,10 +332,8 @@ __device__ __forceinline__ float getimp(const float* si, float pos, float margin
     y = x;
   } else if (p == 2.0f) {  // MuJoCo's default power: no powf (4 divergent powf calls cost ~200 VALU)
     y = (x <= mid) ? x * x / mid : 1.0f - (1.0f - x) * (1.0f - x) / (1.0f - mid);
-  } else if (x <= mid) {
-    y = powf(x, p) / powf(mid, p - 1.0f);
   } else {
-    y = 1.0f - powf(1.0f - x, p) / powf(1.0f - mid, p - 1.0f);
+    y = getimp_pow(x, mid, p);
   }
   return si[0] + y * (si[1] - si[0]);
 }

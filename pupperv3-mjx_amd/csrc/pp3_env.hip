@@ -1379,6 +1379,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   }
   rne_body_forces(s, l, h);
   const int ncon = s.ncon;
+  __builtin_assume(ncon >= 0 && ncon <= NC);  // (collision caps it): NC = 8 -> one edge-row pass
   for (int it = l; it < ncon * NV; it += HW) {
     const int c = it / NV, i = it - c * NV;
     const uint32_t bit = 1u << i;
