@@ -1619,53 +1619,19 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
 #pragma unroll
         for (int j = 0; j < NV; j++) a[j] += (j == lp) ? dD : 0.0f;
         for (int c = 0; c < cmax; c++) {
+          const bool cv = c < ncon;
           const int sa = __builtin_amdgcn_readlane(lsup, c), sb = __builtin_amdgcn_readlane(lsup, HW + c);
-          const int lg = h ? sb : sa;  // this half's contact leg (4: base only)
-          if (c < ncon) {
-            // every operand of the contact in ONE pinned LDS round: G, the lane's J column, the
-            // three base rows and the three rows of this half's leg block (read at the leg's
-            // columns: no per-leg branch, no second round)
-            const float(&J)[3][NV] = s.Jc[c];
-            const int lc = 6 + 3 * (lg < 4 ? lg : 0);
-            v2f g01 = {s.con_G[c][0], s.con_G[c][1]}, g23 = {s.con_G[c][2], s.con_G[c][3]};
-            float g4 = s.con_G[c][4];
-            v2f jd01 = {J[0][dn], J[1][dn]};
-            float jd2 = J[2][dn];
-            v2f jb[3][3], jl[3];
-            float jl2[3];
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-#pragma unroll
-              for (int q = 0; q < 3; q++) jb[k][q] = v2f{J[k][2 * q], J[k][2 * q + 1]};
-              jl[k] = v2f{J[k][lc], J[k][lc + 1]};
-              jl2[k] = J[k][lc + 2];
-            }
-            PIN("+v"(g01), "+v"(g23), "+v"(g4), "+v"(jd01), "+v"(jd2), "+v"(jb[0][0]), "+v"(jb[0][1]), "+v"(jb[0][2]),
-                "+v"(jb[1][0]), "+v"(jb[1][1]), "+v"(jb[1][2]), "+v"(jb[2][0]), "+v"(jb[2][1]), "+v"(jb[2][2]),
-                "+v"(jl[0]), "+v"(jl[1]), "+v"(jl[2]), "+v"(jl2[0]), "+v"(jl2[1]), "+v"(jl2[2]));
-            const float jn = jd01.x, j1 = jd01.y, j2 = jd2;
-            const float w0 = jn * g01.x + j1 * g01.y + j2 * g23.x;
-            const float w1 = jn * g01.y + j1 * g23.y;
-            const float w2 = jn * g23.x + j2 * g4;
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-              const float b0 = (j & 1) ? jb[0][j >> 1].y : jb[0][j >> 1].x;
-              const float b1 = (j & 1) ? jb[1][j >> 1].y : jb[1][j >> 1].x;
-              const float b2 = (j & 1) ? jb[2][j >> 1].y : jb[2][j >> 1].x;
-              a[npos(j)] += w0 * b0 + w1 * b1 + w2 * b2;  // same expression as hess_acc_p
-            }
-            const float l0[3] = {jl[0].x, jl[0].y, jl2[0]}, l1[3] = {jl[1].x, jl[1].y, jl2[1]};
-            const float l2[3] = {jl[2].x, jl[2].y, jl2[2]};
-            float p[3];
-#pragma unroll
-            for (int jj = 0; jj < 3; jj++) p[jj] = w0 * l0[jj] + w1 * l1[jj] + w2 * l2[jj];
-            // a + 1 * p rounds like a + p; a + 0 * p = a (p finite)
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-              const float mg = (lg == g) ? 1.0f : 0.0f;
-#pragma unroll
-              for (int jj = 0; jj < 3; jj++) a[npos(6 + 3 * g + jj)] = fmaf(mg, p[jj], a[npos(6 + 3 * g + jj)]);
-            }
+          if (cv) {
+            const float* G = s.con_G[c];
+            const float jn = s.Jc[c][0][dn], j1 = s.Jc[c][1][dn], j2 = s.Jc[c][2][dn];
+            const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
+            const float w1 = jn * G[1] + j1 * G[3];
+            const float w2 = jn * G[2] + j2 * G[4];
+            hess_acc_p<0, 6>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 0 || sb == 0) hess_acc_p<6, 9>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 1 || sb == 1) hess_acc_p<9, 12>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 2 || sb == 2) hess_acc_p<12, 15>(a, s.Jc[c], w0, w1, w2);
+            if (sa == 3 || sb == 3) hess_acc_p<15, 18>(a, s.Jc[c], w0, w1, w2);
           }
         }
         PHASE(14); l = opaque_lane(l);
