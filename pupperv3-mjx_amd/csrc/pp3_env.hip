@@ -1432,6 +1432,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   }
   }  // AB_REP(12): the bias part only
   const int nl = s.nl;
+  __builtin_assume(nl >= 0 && nl <= NLMAX);
   const int nefc = NFR + nl + 4 * ncon;
   for (int e = l; e < 4 * ncon; e += HW) {
     const int c = e >> 2, p = s.con_pair[c], r = NFR + nl + e;
@@ -1530,6 +1531,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   SYNC();
   PHASE(5); l = opaque_lane(l);
   const int cmax = wmax2(ncon);
+  __builtin_assume(cmax >= 0 && cmax <= NC);
   int weight = cmax;  // returned: the wave's load this substep (contacts, +2 on the leg-leg path)
   bool live = true;  // this env still iterating (per half)
   for (int iter = 0; iter < m.iterations; iter++) {
