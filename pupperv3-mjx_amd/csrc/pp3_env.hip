@@ -439,20 +439,26 @@ __device__ __forceinline__ void make_frame(float f[9], const float nin[3]) {
 
 // narrow phase for pair p; returns hit and fills dist/pos/normal.  One dependent global level:
 // the pair's flattened record (PairRec), then robot-geom world positions from LDS.
+// the pair record (6 x 16 B) and the first word group of its PairCon (for store_contact): one
+// batch of loads
+struct PairLoad {
+  v4f v[7];
+};
+__device__ __forceinline__ PairLoad load_pair(const DevModel& m, int p) {
+  PairLoad r;
+#pragma unroll
+  for (int k = 0; k < 6; k++) r.v[k] = *reinterpret_cast<const v4f*>(m.pair_rec.g[k][p]);
+  r.v[6] = *reinterpret_cast<const v4f*>(&m.pair_con[p]);
+  return r;
+}
 template <int NC>
-__device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, int p, float& dist, float pos[3],
+__device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, PairLoad pl, float& dist, float pos[3],
                                        float nrm[3], v4f& pc0) {
-  // the pair record (6 x 16 B) and the first word group of its PairCon (for store_contact) in
-  // one batch of loads
   PairRec rec;
   {
-    v4f v[7];
-#pragma unroll
-    for (int k = 0; k < 6; k++) v[k] = *reinterpret_cast<const v4f*>(m.pair_rec.g[k][p]);
-    v[6] = *reinterpret_cast<const v4f*>(&m.pair_con[p]);
-    PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]));
-    __builtin_memcpy(&rec, v, sizeof(rec));
-    pc0 = v[6];
+    PIN("+v"(pl.v[0]), "+v"(pl.v[1]), "+v"(pl.v[2]), "+v"(pl.v[3]), "+v"(pl.v[4]), "+v"(pl.v[5]), "+v"(pl.v[6]));
+    __builtin_memcpy(&rec, pl.v, sizeof(rec));
+    pc0 = pl.v[6];
   }
   const float margin = rec.margin;
   float p1[3], p2[3];
@@ -555,13 +561,15 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const v4f& pc0, int
 // contact support (pair_sup of contact c; 4 = no contact): the Newton phases read contact
 // supports with v_readlane from this register instead of LDS round trips per contact.
 template <int NC>
-__device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h) {
+__device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h, const PairLoad& pre) {
   int nhit = 0;
   for (int base = 0; base < m.npair; base += HW) {
     const int p = base + l;
     float dist = 0, pos[3], nrm[3];
     v4f pc0;
-    const bool hit = narrow(s, m, p < m.npair ? p : 0, dist, pos, nrm, pc0) && (p < m.npair);
+    // the first 32 pairs' records were fetched at the substep start (they arrive during kinematics)
+    const PairLoad pl = base == 0 ? pre : load_pair(m, p < m.npair ? p : 0);
+    const bool hit = narrow(s, m, pl, dist, pos, nrm, pc0) && (p < m.npair);
     const uint32_t mask = hballot(hit, h);
     const int slot = nhit + __popc(mask & ((1u << l) - 1u));
     if (hit) {
@@ -607,7 +615,7 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
       if (keep[t]) {
         float dist, pos[3], nrm[3];
         v4f pc0;
-        narrow(s, m, keep_p[t], dist, pos, nrm, pc0);
+        narrow(s, m, load_pair(m, keep_p[t]), dist, pos, nrm, pc0);
         store_contact(s, pc0, slot[t], keep_p[t], dist, pos, nrm);
       }
     }
@@ -1290,6 +1298,8 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     for (int k = 0; k < 3; k++)
       for (int c = 0; c < 4; c++) rm_pf.f[4 * k + c] = v[2 + k][c];
   }
+  // the narrow phase's pair records for this lane's first pair, likewise (model constants)
+  const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
   AB_REP(1) { kinematics(s, m, l); SYNC(); }
   PHASE(0); l = opaque_lane(l);
   AB_REP(2) { com_pos(s, m, l, h, rc_pf); SYNC(); }
@@ -1298,7 +1308,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   AB_REP(3) { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
   int lsup = 4;  // lane c: support of contact c (4 = none)
-  AB_REP(4) { lsup = collision(s, m, l, h); SYNC(); }
+  AB_REP(4) { lsup = collision(s, m, l, h, pair_pf); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   // the PairCon of contact c = l / 4 for the first batch of phase 13's edge rows (lane e = 4c + k),
   // loaded here unpinned: it arrives during the limit/actuation and M-entry phases
