@@ -3,7 +3,8 @@
 configs[1]: 4096 envs (2048 one-wave workgroups: every CU holds a full generation), flat,
 fixed command (0.5, 0, 0), no DR.  configs[3] per GPU: 8192 envs (two generations), commands
 sampled at reset and resampled every 500 steps.  Plus an odd batch (4097: the last wave's
-second half recomputes env N-1 and must store nothing).
+second half recomputes env N-1 and must store nothing).  configs[0] (1 env, zero command,
+mj_step plumbing) runs as C1 below: 1000 free-running env steps against the fp64 oracle.
 
 20 env steps of U(-1,1) actions each; property checks on every env (finite, obs within the clip,
 shapes, done/reward ranges, RNG words advanced and pairwise distinct), then one further step
@@ -13,6 +14,7 @@ and the last workgroup included -- with the same per-term tolerances as test_gpu
 import numpy as np
 import pytest
 
+import common
 import gpu_harness as G
 from bench import bench_kwargs
 from oracle import oracle as O
@@ -94,3 +96,50 @@ def test_configs3_8192_envs_random_commands(require_gpu):
 
 def test_odd_batch_4097_envs(require_gpu):
     _run(require_gpu, 4097, False, "headline_4097")
+
+
+def test_configs0_c1_zero_command_1000_steps(require_gpu):
+    """configs[0] at env level: 1 env, flat, command (0,0,0) fixed (zero
+    ranges, no orientation command), observation noise, kick and latencies off (latency [1], IMU
+    latency [1]), actions 0, 1000 env steps (5000 substeps) FREE-RUNNING on the kernel and on the
+    fp64 oracle from the same reset key; qpos / qvel / obs compared at every step.  The fp32 oracle,
+    run alongside, calibrates the tolerance: the kernel may drift from fp64 by at most 10x what a
+    plain fp32 execution of the same algorithm drifts, floored at 1e-4 (qpos) / 1e-3 (qvel)."""
+    kw = common.fixture_kwargs(MODEL_XML, angular_velocity_noise=0.0, gravity_noise=0.0, motor_angle_noise=0.0,
+                               last_action_noise=0.0, kick_probability=0.0, latency_distribution=[1.0],
+                               imu_latency_distribution=[1.0], linear_velocity_x_range=[0.0, 0.0],
+                               linear_velocity_y_range=[0.0, 0.0], angular_velocity_range=[0.0, 0.0],
+                               maximum_pitch_command=0.0, maximum_roll_command=0.0)
+    env = PupperV3Env(**kw, num_envs=1)
+    try:
+        key = make_keys(0, 1)
+        st = env.reset(key)
+        o64 = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f64")
+        o32 = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f32")
+        s64, s32 = o64.reset(key[0]), o32.reset(key[0])
+        np.testing.assert_allclose(st._record[0, :19], G.oracle_state_to_record(s64["state"])[:19], atol=1e-6)
+        zero = np.zeros(12)
+        worst = dict(qpos=0.0, qvel=0.0, obs=0.0, qpos32=0.0, qvel32=0.0)
+        for t in range(1000):
+            st = env.step(st, np.zeros((1, 12), dtype=np.float32))
+            s64, s32 = o64.step(s64, zero), o32.step(s32, zero)
+            g, r64 = st._record[0], G.oracle_state_to_record(s64["state"])
+            r32 = G.oracle_state_to_record(s32["state"])
+            qv = slice(_abi.S_QVEL, _abi.S_QVEL + 18)
+            worst["qpos"] = max(worst["qpos"], float(np.abs(g[:19] - r64[:19]).max()))
+            worst["qvel"] = max(worst["qvel"], float(np.abs(g[qv] - r64[qv]).max()))
+            worst["obs"] = max(worst["obs"], float(np.abs(st.obs[0] - s64["obs"]).max()))
+            worst["qpos32"] = max(worst["qpos32"], float(np.abs(r32[:19] - r64[:19]).max()))
+            worst["qvel32"] = max(worst["qvel32"], float(np.abs(r32[qv] - r64[qv]).max()))
+            assert st.done[0] == s64["done"] == 0, t  # it stands: no termination, no reset
+            assert np.all(st.info["command"] == 0.0)
+        G.report("configs0_c1", {"steps": 1000, "worst": {k: float(f"{v:.3g}") for k, v in worst.items()}})
+        assert worst["qpos"] <= max(1e-4, 10 * worst["qpos32"]), worst
+        assert worst["qvel"] <= max(1e-3, 10 * worst["qvel32"]), worst
+        assert worst["obs"] <= 5e-3, worst
+        # it stood up from the drop and stays standing: base height and tilt at the end
+        q = st._record[0, :7]
+        up_z = 1.0 - 2.0 * (q[4] ** 2 + q[5] ** 2)  # world z of the body z axis (quat w, x, y, z at 3..6)
+        assert 0.1 < q[2] < 0.3 and up_z > 0.9, q
+    finally:
+        env.close()
