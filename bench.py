@@ -325,6 +325,10 @@ def main():
     env.synchronize()
     barrier()
     wall = time.perf_counter() - t0
+    # the rollout's end state (rank 0's shard): equal hashes across kernel builds mean the A/B
+    # variants ran the same trajectories, so a timing difference is code speed, not a changed workload
+    import hashlib
+    state_sha16 = hashlib.sha256(env._get(_abi.F_STATE).tobytes()).hexdigest()[:16]
     gather_info = None
     if args.gather:
         # untimed: the same K steps' kernels alone (events), then the gather alone
@@ -374,6 +378,7 @@ def main():
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / K * 1e3, 4),
+            "state_sha16": state_sha16,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
