@@ -230,7 +230,16 @@ def main():
     from pupperv3_mjx import MODEL_XML, _abi, _lib, sharding
     from pupperv3_mjx.environment import PupperV3Env
 
-    comm = sharding.Comm(rank, world, device) if world > 1 else None
+    comm, comm_kind = None, None
+    if world > 1:
+        try:
+            comm, comm_kind = sharding.Comm(rank, world, device), "RCCL (pp3_comm)"
+        except Exception as exc:  # timing still needs a barrier + max over ranks; the shards never exchange data
+            if args.gather:
+                raise
+            print(f"rank {rank}: RCCL communicator unavailable ({exc}); barrier/max-over-ranks through files",
+                  file=sys.stderr, flush=True)
+            comm, comm_kind = sharding.FileComm(rank, world), "host files (RCCL init failed)"
 
     model_path = MODEL_XML
     if args.obstacles:
@@ -393,7 +402,7 @@ def main():
                        if not args.gather else f"env-sharded x{world} + per-step RCCL gather to rank {args.gather_root}",
                        "per_env_terrain": bool(args.terrain),
                        "commands": "reset-sampled, resampled every 500 steps" if args.random_commands else "fixed (0.5,0,0)",
-                       "gather": gather_info, "auto_reset_episode_length": args.auto_reset or None,
+                       "gather": gather_info, "comm": comm_kind, "auto_reset_episode_length": args.auto_reset or None,
                        "policy_in_loop": args.policy or None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,

@@ -71,6 +71,9 @@ def unpack_gathered(full, global_envs: int, world: int):
 
 
 # ------------------------------------------------------------------------------ rendezvous
+_RDZV_ERR = b"PP3_RDZV_ERROR:"  # (an id is COMM_ID_BYTES of binary; this prefix marks rank 0's failure)
+
+
 def _rdzv_path(tag: str) -> str:
     """Per-launch file name on the node.  Explicit PP3_RDZV_FILE wins (e.g. a shared file system
     for several nodes); under torch.distributed.run every worker of one launch has the same
@@ -90,17 +93,26 @@ def rendezvous_id(rank: int, world: int, make_id: Callable[[], bytes], tag: str 
     the node; the other ranks poll for it.  Returns the id on every rank."""
     path = _rdzv_path(tag)
     if rank == 0:
-        blob = bytes(make_id())
+        err = None
+        try:
+            blob = bytes(make_id())
+        except Exception as exc:  # published too, so the other ranks fail now instead of at their timeout
+            err = exc
+            blob = _RDZV_ERR + str(exc).encode()
         tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "wb") as f:
             f.write(blob)
         os.replace(tmp, path)  # atomic publish
+        if err is not None:
+            raise err
         return blob
     t0 = time.monotonic()
     while True:
         try:
             with open(path, "rb") as f:
                 blob = f.read()
+            if blob.startswith(_RDZV_ERR):
+                raise RuntimeError(f"rank 0 could not create the communicator id: {blob[len(_RDZV_ERR):].decode()}")
             if blob:
                 return blob
         except FileNotFoundError:
@@ -180,3 +192,66 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+class FileComm:
+    """Host-only stand-in for ``Comm``'s barrier and reductions (no gather), through files in one
+    directory on the node.  bench.py falls back to it when the RCCL communicator cannot be
+    created, so a multi-GPU timing run still gets its barrier and max-over-ranks timing; the env
+    shards themselves never exchange data.  Round k: every rank publishes its values atomically
+    as ``<dir>/<k>.<rank>`` and polls until all ``world`` files of round k exist."""
+
+    def __init__(self, rank: int, world: int, tag: str = "_file", timeout_s: float = 300.0,
+                 directory: Optional[str] = None):
+        self.rank, self.world = int(rank), int(world)
+        self._dir = directory or (_rdzv_path(tag) + ".d")
+        os.makedirs(self._dir, exist_ok=True)
+        self._round = 0
+        self._timeout = timeout_s
+
+    def _exchange(self, values) -> np.ndarray:
+        k = self._round
+        self._round += 1
+        v = np.ascontiguousarray(values, dtype=np.float64).ravel()
+        path = os.path.join(self._dir, f"{k}.{self.rank}")
+        with open(path + ".tmp", "wb") as f:
+            f.write(v.tobytes())
+        os.replace(path + ".tmp", path)
+        out = np.empty((self.world, v.size))
+        t0 = time.monotonic()
+        for r in range(self.world):
+            p = os.path.join(self._dir, f"{k}.{r}")
+            while not os.path.exists(p):
+                if time.monotonic() - t0 > self._timeout:
+                    raise TimeoutError(f"rank {self.rank}: rank {r} missing from round {k} at {self._dir}")
+                time.sleep(2e-5)
+            with open(p, "rb") as f:
+                out[r] = np.frombuffer(f.read(), dtype=np.float64)
+        if k >= 2:  # every rank has finished round k - 1 (it published round k): drop own k - 2
+            try:
+                os.remove(os.path.join(self._dir, f"{k - 2}.{self.rank}"))
+            except FileNotFoundError:
+                pass
+        return out
+
+    def allreduce(self, values, op: str = "max") -> np.ndarray:
+        a = self._exchange(values)
+        return a.max(0) if op == "max" else a.sum(0)
+
+    def barrier(self) -> None:
+        self._exchange([0.0])
+
+    def gather(self, *args, **kwargs) -> None:
+        raise RuntimeError("FileComm has no device gather: --gather needs the RCCL communicator")
+
+    def close(self) -> None:
+        if self._dir is None:
+            return
+        # after this last round every rank has read the previous one: drop it; the last round's
+        # files stay (a slower rank may still be reading them), a few bytes per rank in the directory
+        self.barrier()
+        try:
+            os.remove(os.path.join(self._dir, f"{self._round - 2}.{self.rank}"))
+        except FileNotFoundError:
+            pass
+        self._dir = None

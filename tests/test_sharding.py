@@ -147,3 +147,69 @@ def test_sharding_module_is_torch_free():
              for a in n.names}
     mods = {n.module for n in ast.walk(ast.parse(src)) if isinstance(n, ast.ImportFrom) and n.module}
     assert not any(x.split(".")[0] == "torch" for x in names | mods)
+
+
+def _rdzv_fail_worker(rank, world, d, ret):
+    os.environ["PP3_RDZV_DIR"] = d
+    os.environ["MASTER_PORT"] = "4343"
+
+    def bad_id():
+        raise RuntimeError("no librccl here")
+    try:
+        sharding.rendezvous_id(rank, world, bad_id, tag="_fail", timeout_s=30)
+        ret[rank] = "ok"
+    except Exception as exc:  # every rank must fail fast, not at its timeout
+        ret[rank] = type(exc).__name__ + ":" + str(exc)
+
+
+def test_rendezvous_failure_reaches_every_rank(tmp_path):
+    """Rank 0's failure to create the id is published, so the other ranks raise at once (bench.py
+    then falls back to FileComm on every rank instead of rank 0 waiting out the others' timeout)."""
+    import multiprocessing as mpc
+    import time
+    t0 = time.monotonic()
+    with mpc.Manager() as mgr:
+        ret = mgr.dict()
+        ps = [mpc.Process(target=_rdzv_fail_worker, args=(r, 2, str(tmp_path), ret)) for r in (1, 0)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(60)
+        out = dict(ret)
+    assert time.monotonic() - t0 < 20
+    assert out[0].startswith("RuntimeError:") and "no librccl" in out[0]
+    assert out[1].startswith("RuntimeError:") and "no librccl" in out[1]
+
+
+def _filecomm_worker(rank, world, d, ret):
+    fc = sharding.FileComm(rank, world, directory=d, timeout_s=30)
+    res = []
+    for k in range(5):
+        res.append(fc.allreduce([rank + k, -rank], "max").tolist())
+        fc.barrier()
+        res.append(fc.allreduce([rank + k], "sum").tolist())
+    fc.close()
+    ret[rank] = res
+
+
+def test_file_comm_barrier_and_reductions(tmp_path):
+    """The host-file fallback of bench.py's barrier / max-over-ranks timing, 3 processes."""
+    import multiprocessing as mpc
+    world = 3
+    with mpc.Manager() as mgr:
+        ret = mgr.dict()
+        ps = [mpc.Process(target=_filecomm_worker, args=(r, world, str(tmp_path), ret)) for r in (2, 0, 1)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(60)
+            assert p.exitcode == 0
+        out = [ret[r] for r in range(world)]
+    expect = []
+    for k in range(5):
+        expect.append([world - 1 + k, 0.0])
+        expect.append([sum(r + k for r in range(world))])
+    for r in range(world):
+        assert out[r] == expect
+    # only the last round's files are left behind
+    assert len(os.listdir(tmp_path)) == world
