@@ -256,6 +256,51 @@ class PupperV3Env:
         self._act_buf = _lib.DeviceBuffer(self.num_envs * _abi.NU * 4, self.device)
         self._dr_buf = None
 
+    # ------------------------------------------------------------------ reference helpers
+    def sample_command(self, rng) -> np.ndarray:
+        """environment.py:246-272 on the host: one key [2] or a batch [..., 2] -> f32[..., 3]
+        (lin_vel_x, lin_vel_y, ang_vel_yaw), near zero with probability zero_command_probability.
+        The same jax.random draws as the device's reset / resample (env_step_kernel
+        sample_command), so a key gives the identical command."""
+        c, p = self.config_struct, self._partitionable
+        k = _rng.split(np.asarray(rng, dtype=np.uint32), 6, p)
+        f = np.float32
+        vx = _rng.uniform(k[..., 1, :], (1,), f(c.lin_vel_x_range[0]), f(c.lin_vel_x_range[1]), p)[..., 0]
+        vy = _rng.uniform(k[..., 2, :], (1,), f(c.lin_vel_y_range[0]), f(c.lin_vel_y_range[1]), p)[..., 0]
+        wz = _rng.uniform(k[..., 3, :], (1,), f(c.ang_vel_range[0]), f(c.ang_vel_range[1]), p)[..., 0]
+        pz = _rng.uniform(k[..., 4, :], (1,), partitionable=p)[..., 0]
+        thr = f(c.stand_still_command_threshold)
+        near_zero = _rng.uniform(k[..., 5, :], (3,), -thr, thr, p)
+        cmd = np.stack([vx, vy, wz], axis=-1)
+        return np.where((pz < f(c.zero_command_probability))[..., None], near_zero, cmd).astype(np.float32)
+
+    def sample_body_orientation(self, rng) -> np.ndarray:
+        """environment.py:274-298 on the host: the desired world z in the body frame rotated by a
+        random roll / pitch (brax math.euler_to_quat in degrees, then math.rotate), f32[..., 3]."""
+        c, p = self.config_struct, self._partitionable
+        k = _rng.split(np.asarray(rng, dtype=np.uint32), 3, p)
+        f = np.float32
+        pitch = _rng.uniform(k[..., 1, :], (1,), f(-1), f(1), p)[..., 0] * f(c.max_pitch_command)
+        roll = _rng.uniform(k[..., 2, :], (1,), f(-1), f(1), p)[..., 0] * f(c.max_roll_command)
+        h1, h2 = roll * f(np.pi / 360), pitch * f(np.pi / 360)  # half angles (yaw 0)
+        c1, s1, c2, s2 = np.cos(h1), np.sin(h1), np.cos(h2), np.sin(h2)
+        q = np.stack([c1 * c2, s1 * c2, c1 * s2, s1 * s2], axis=-1).astype(np.float32)
+        v = np.broadcast_to(np.asarray(c.desired_world_z[:], dtype=np.float32), q.shape[:-1] + (3,))
+        s, u = q[..., :1], q[..., 1:]
+        r = 2 * np.sum(u * v, -1, keepdims=True) * u + (s * s - np.sum(u * u, -1, keepdims=True)) * v
+        return (r + 2 * s * np.cross(u, v)).astype(np.float32)
+
+    def initial_action_buffer(self) -> np.ndarray:
+        """environment.py:300-301: zeros [12, len(latency_distribution)]."""
+        return np.zeros((_abi.NU, len(self._latency_distribution)), dtype=np.float32)
+
+    def initial_imu_buffer(self) -> np.ndarray:
+        """environment.py:303-312: [6, len(imu_latency_distribution)] zeros with gravity z = -1
+        (rows: angular velocity xyz, gravity xyz)."""
+        buf = np.zeros((6, len(self._imu_latency_distribution)), dtype=np.float32)
+        buf[5, :] = -1.0
+        return buf
+
     # ------------------------------------------------------------------ properties
     @property
     def dt(self) -> float:
