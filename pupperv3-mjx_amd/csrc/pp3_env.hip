@@ -3139,6 +3139,8 @@ int pp3_device_count(void) {
   return n;
 }
 
+static int alloc_env_buffers(pp3_env* e, const DevModel& hm);
+
 int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t num_envs, int32_t device, pp3_env_t** out) {
   if (!model || !cfg || !out || num_envs < 1) return set_err(PP3_ERR_ARG, "bad arguments to pp3_create");
   DevModel hm;
@@ -3146,8 +3148,8 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   if (rc) return rc;
   HIPCHK(hipSetDevice(device));
   pp3_env* e = new pp3_env();
-  e->action_repeat = 1;
   memset(e, 0, sizeof(*e));
+  e->action_repeat = 1;
   e->device = device;
   e->N = num_envs;
   e->stride = hm.stride;
@@ -3162,7 +3164,18 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
       return set_err(PP3_ERR_ARG, "ncon_max must be 0 (auto), 8 or 16");
     }
   }
-  const size_t N = (size_t)num_envs;
+  rc = alloc_env_buffers(e, hm);
+  if (rc) {
+    pp3_destroy(e);  // frees what was allocated (hipFree(nullptr) is a no-op)
+    return rc;
+  }
+  *out = e;
+  return PP3_OK;
+}
+
+// device buffers of a new handle (pp3_create); on failure the caller destroys the handle
+static int alloc_env_buffers(pp3_env* e, const DevModel& hm) {
+  const size_t N = (size_t)e->N;
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   HIPCHK(hipMalloc(&e->dmodel, sizeof(DevModel)));
   HIPCHK(hipMemcpy(e->dmodel, &hm, sizeof(DevModel), hipMemcpyHostToDevice));
@@ -3180,20 +3193,19 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   HIPCHK(hipMemset(e->action, 0, N * PP3_NU * sizeof(float)));
   HIPCHK(hipEventCreate(&e->ev0));
   HIPCHK(hipEventCreate(&e->ev1));
-  *out = e;
   return PP3_OK;
 }
 
 int pp3_destroy(pp3_env_t* e) {
   if (!e) return PP3_OK;
   (void)hipSetDevice(e->device);
-  (void)hipStreamSynchronize(e->stream);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->dmodel, e->state, e->obs, e->reward, e->done, e->metrics, e->dr, e->pipe, e->action,
                   e->episode, e->first_state, e->first_obs, e->terrain};
   for (void* b : bufs) (void)hipFree(b);
-  (void)hipEventDestroy(e->ev0);
-  (void)hipEventDestroy(e->ev1);
-  (void)hipStreamDestroy(e->stream);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return PP3_OK;
 }
@@ -3393,6 +3405,7 @@ int pp3_copy_field_to_host(pp3_env_t* e, int32_t field, void* host, size_t bytes
   int rc = pp3_field(e, field, &p, &n);
   if (rc) return rc;
   if (bytes != (size_t)n * e->N * 4) return set_err(PP3_ERR_ARG, "pp3_copy_field_to_host: size mismatch");
+  if (!p) return set_err(PP3_ERR_ARG, "pp3_copy_field_to_host: field not allocated (auto-reset fields need pp3_set_auto_reset)");
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(host, p, bytes, hipMemcpyDeviceToHost));
@@ -3405,6 +3418,7 @@ int pp3_copy_field_from_host(pp3_env_t* e, int32_t field, const void* host, size
   int rc = pp3_field(e, field, &p, &n);
   if (rc) return rc;
   if (bytes != (size_t)n * e->N * 4) return set_err(PP3_ERR_ARG, "pp3_copy_field_from_host: size mismatch");
+  if (!p) return set_err(PP3_ERR_ARG, "pp3_copy_field_from_host: field not allocated (auto-reset fields need pp3_set_auto_reset)");
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(p, host, bytes, hipMemcpyHostToDevice));

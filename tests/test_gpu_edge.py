@@ -262,3 +262,21 @@ def test_create_rejects_two_sided_limit_margin(require_gpu):
     m.jnt_margin[3] = 0.6 * (m.jnt_range[3][1] - m.jnt_range[3][0])
     with pytest.raises(_lib.PupperHipError, match="twice the margin"):
         G.env_with_model(common.MODEL_XML, m, 2)
+
+
+def test_unallocated_field_copy_and_bad_create_fail_loudly(box_path):
+    """Auto-reset fields exist only after pp3_set_auto_reset: copying one before raises instead of
+    reading a null device pointer; a pp3_create that fails (bad contact cap) leaves nothing behind
+    and the next create works."""
+    from pupperv3_mjx import _lib
+    env = PupperV3Env(**common.fixture_kwargs(box_path), num_envs=3)
+    try:
+        out = np.empty((3, _abi.EP_STRIDE), dtype=np.float32)
+        with pytest.raises(_lib.PupperHipError, match="not allocated"):
+            _lib.check(env._L.pp3_copy_field_to_host(env._h, _abi.F_EPISODE, out.ctypes.data_as(_lib.C.c_void_p),
+                                                     out.nbytes))
+    finally:
+        env.close()
+    with pytest.raises(_lib.PupperHipError, match="ncon_max"):
+        PupperV3Env(**common.fixture_kwargs(box_path), num_envs=3, max_contacts=12)
+    PupperV3Env(**common.fixture_kwargs(box_path), num_envs=3).close()
