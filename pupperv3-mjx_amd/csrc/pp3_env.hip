@@ -645,16 +645,21 @@ __device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int 
       "+v"(lcd[1][0]), "+v"(lcd[1][1]), "+v"(lcd[1][2]), "+v"(lcd[1][3]), "+v"(lcd[1][4]), "+v"(lcd[1][5]),
       "+v"(lcd[2][0]), "+v"(lcd[2][1]), "+v"(lcd[2][2]), "+v"(lcd[2][3]), "+v"(lcd[2][4]), "+v"(lcd[2][5]),
       "+v"(lqd[0]), "+v"(lqd[1]), "+v"(lqd[2]));
-  float cv[6] = {0, 0, 0, 0, 0, 0}, ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
-  for (int d = 0; d < 3; d++)
-    for (int k = 0; k < 6; k++) cv[k] += s.cdof[d][k] * s.qvel[d];
-  float cdd[6];
+  // free joint in closed form: its translational cdof are the unit vectors (com_pos), so the
+  // velocity after them is (0, v); each rotational dof's cdof_dot = (0, v) x cdof = (0, v x a_d),
+  // hence cacc = (0, -g + v x w) with w = sum_d a_d qvel[3+d], and cvel = (w, v + sum_d b_d qvel[3+d])
+  float w[3] = {0, 0, 0}, bsum[3] = {0, 0, 0};
+#pragma unroll
   for (int d = 0; d < 3; d++) {
-    cross_motion(cdd, cv, s.cdof[3 + d]);
-    for (int k = 0; k < 6; k++) ca[k] += cdd[k] * s.qvel[3 + d];
+    const float q = s.qvel[3 + d];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { w[k] += s.cdof[3 + d][k] * q; bsum[k] += s.cdof[3 + d][3 + k] * q; }
   }
-  for (int d = 0; d < 3; d++)
-    for (int k = 0; k < 6; k++) cv[k] += s.cdof[3 + d][k] * s.qvel[3 + d];
+  const float v0 = s.qvel[0], v1 = s.qvel[1], v2 = s.qvel[2];
+  float cv[6] = {w[0], w[1], w[2], v0 + bsum[0], v1 + bsum[1], v2 + bsum[2]};
+  float ca[6] = {0, 0, 0, -m.gravity[0] + (v1 * w[2] - v2 * w[1]), -m.gravity[1] + (v2 * w[0] - v0 * w[2]),
+                 -m.gravity[2] + (v0 * w[1] - v1 * w[0])};
+  float cdd[6];
   if (l == 0)
     for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv[k]; s.x.a.cacc[1][k] = ca[k]; }
 #pragma unroll
