@@ -246,7 +246,7 @@ __device__ __forceinline__ int wmax2(int v) {
 // Hinge anchors coincide with body origins (jnt_pos = 0, checked at pp3_create).
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l) {
+__device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l, bool euler) {
   // every model constant of the phase is fetched up front (clamped lane indices, no branches)
   // and pinned by one asm statement: one vmcnt wait instead of one per dependent use
   const int lc = l < 12 ? l : 11, gl = lc & 3, kl = lc >> 2;
@@ -270,12 +270,44 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
       "+v"(bpos[1][2]), "+v"(bpos[2][0]), "+v"(bpos[2][1]), "+v"(bpos[2][2]), "+v"(jaxc[0][0]),
       "+v"(jaxc[0][1]), "+v"(jaxc[0][2]), "+v"(jaxc[1][0]), "+v"(jaxc[1][1]), "+v"(jaxc[1][2]),
       "+v"(jaxc[2][0]), "+v"(jaxc[2][1]), "+v"(jaxc[2][2]));
-  float lq[4] = {1, 0, 0, 0};
-  if (l < 12) {
-    float qloc[4];
-    axisangle2quat(qloc, jax, s.qpos[ql] - q0);
-    mulquat(lq, bq, qloc);
+  // The previous substep's Euler step (eulerdamp disabled), deferred to here when `euler`: the
+  // joint lanes integrate their own dof (so the new angle stays in a register), lanes 12..17 the
+  // base dofs, and lane 15 integrates the base quaternion -- its axis-angle rotation shares the
+  // joints' sincos instructions instead of a serial sequence of its own (same arithmetic as
+  // euler_step, which integrates the last substep).
+  float qj = s.qpos[ql], aax[3] = {jax[0], jax[1], jax[2]}, ang = 0.0f, qb[4];
+  if (euler) {
+    const float hstep = m.h;
+    const int d = l < 12 ? ql - 1 : l - 12;  // the dof this lane integrates (l < 18)
+    float vn = 0.0f, w[3] = {0, 0, 0};
+    if (l < 18) vn = s.qvel[d] + hstep * s.qacc[d];
+    if (l == 15)
+      for (int k = 0; k < 3; k++) w[k] = s.qvel[3 + k] + hstep * s.qacc[3 + k];
+    for (int k = 0; k < 4; k++) qb[k] = s.qpos[3 + k];
+    SYNC();
+    if (l < 18) s.qvel[d] = vn;
+    if (l < 12) { qj += hstep * vn; s.qpos[ql] = qj; }
+    if (l >= 12 && l < 15) s.qpos[l - 12] += hstep * vn;
+    if (l == 15) {
+      const float n = sqrtf(dot3(w, w));
+      if (n < MINVAL) { w[0] = 1; w[1] = 0; w[2] = 0; } else { const float in = 1.0f / n; w[0] *= in; w[1] *= in; w[2] *= in; }
+      aax[0] = w[0]; aax[1] = w[1]; aax[2] = w[2];
+      ang = hstep * n;
+    }
   }
+  if (l < 12) ang = qj - q0;
+  float lq[4] = {1, 0, 0, 0};
+  {
+    float qloc[4];
+    axisangle2quat(qloc, aax, ang);
+    if (l < 12) mulquat(lq, bq, qloc);
+    if (euler && l == 15) {
+      normalize4(qb);
+      mulquat(qb, qb, qloc);
+      for (int k = 0; k < 4; k++) s.qpos[3 + k] = qb[k];
+    }
+  }
+  SYNC();  // the base position / quaternion stores above precede the chain lanes' reads below
   // the 3 levels of this lane's leg (lanes 0..3 consume); width-32 shuffles stay in the half
   float lq1[4], lq2[4];
 #pragma unroll
@@ -1277,7 +1309,7 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate PROF_PARAM) {
+__device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
   l = opaque_lane(l);
   // timing ablation only (-DPP3_AB_DUP=k, tools/ab_build.sh): phase k runs twice (the phases so
@@ -1305,7 +1337,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   }
   // the narrow phase's pair records for this lane's first pair, likewise (model constants)
   const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
-  AB_REP(1) { kinematics(s, m, l); SYNC(); }
+  kinematics(s, m, l, integrate_prev); SYNC();
   PHASE(0); l = opaque_lane(l);
   AB_REP(2) { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
@@ -1827,8 +1859,13 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   // the next substep rebuilds its rows)
   if (l < NV) s.efc_aref[l] = s.qvel[l];
   SYNC();
-  if (!integrate) return weight;
-  // ---- phase 8: Euler (eulerdamp disabled) ----
+  return weight;  // the Euler step follows in the next substep's kinematics or in euler_step
+}
+
+// ---- phase 8: Euler (eulerdamp disabled) of the last substep of a step (the earlier ones run
+// fused into the next substep's kinematics) ----
+template <int NC>
+__device__ __forceinline__ void euler_step(Shared<NC>& s, const DevModel& m, int l) {
   const float hstep = m.h;
   float vn = 0;
   float w[3] = {0, 0, 0};
@@ -1849,8 +1886,6 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     for (int k = 0; k < 4; k++) s.qpos[3 + k] = q[k];
   }
   SYNC();
-  PHASE(9);
-  return weight;
 }
 
 // ------------------------------------------------------------------------------------
@@ -2279,8 +2314,14 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    const int wgt = substep(s, *(const DevModel*)mp, l, h, true PROF_ARG);
+    const int wgt = substep(s, *(const DevModel*)mp, l, h, f > 0 PROF_ARG);
     heavy = wgt >= PP3_HEAVY2 ? 2 : (wgt >= PP3_HEAVY ? 1 : 0);
+  }
+  if (n_frames > 0) {  // the last substep's Euler step (the others ran inside the next kinematics)
+    const GModel* mp = (const GModel*)(a.m);
+    asm volatile("" : "+s"(mp));
+    euler_step(s, *(const DevModel*)mp, l);
+    PHASE(9);
   }
   if (heavy) __builtin_amdgcn_s_setprio(3);  // the epilogue: heavy waves, then the younger slot, ahead
   else if (wslot) __builtin_amdgcn_s_setprio(1);
@@ -2625,8 +2666,9 @@ __global__ __launch_bounds__(WAVE, 2) void physics_kernel(PhysArgs a) {
   for (int i = 0; i < a.nsteps; i++) {
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    substep(s, *(const DevModel*)mp, l, h, true PROF_NULL);
+    substep(s, *(const DevModel*)mp, l, h, i > 0 PROF_NULL);
   }
+  if (a.nsteps > 0) euler_step(s, m, l);
   if (!own) return;
   if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
   if (l < NQ) gst[PP3_S_QPOS + l] = s.qpos[l];
