@@ -80,9 +80,12 @@ def _oracle_record(rec):
     return out
 
 
-def one_step_err(env, n_sample=256, seed=0):
+def one_step_err(env, n_sample=256, seed=0, dr_table=None, terrain=None, auto_reset=False):
     """SURVEY 7 hard part 2: one env step (n_frames substeps) of the fp32 kernel vs the fp64 oracle
-    restatement from IDENTICAL states, on the workload's own states after the timed run."""
+    restatement from IDENTICAL states, on the workload's own states after the timed run.  Each
+    sampled env is checked against an oracle env built on ITS model: its domain-randomisation row
+    (`dr_table`) and its terrain (`terrain`).  With auto-reset on, envs that ended their episode in
+    this step hold the episode's first state, not a physics step: they are left out (counted)."""
     import numpy as np
     from pupperv3_mjx import _abi, _lib
     from oracle import oracle as O
@@ -95,11 +98,19 @@ def one_step_err(env, n_sample=256, seed=0):
     env.step_device(buf.ptr.value)
     env.synchronize()
     rec1 = env._get(_abi.F_STATE)
+    done = env._get(_abi.F_DONE).reshape(E) != 0
     buf.free()
     ids = np.random.RandomState(seed + 1).choice(E, size=min(n_sample, E), replace=False)
-    oe = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f64")
+    n_reset = int(done[ids].sum()) if auto_reset else 0
+    if auto_reset:
+        ids = ids[~done[ids]]
+    base = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f64")
     dq, dv, rq, flagged = [], [], [], []
     for i in ids:
+        oe = base
+        if dr_table is not None or terrain is not None:
+            m = env.sys_model.struct if terrain is None else O.model_with_terrain(env.sys_model.struct, terrain[i])
+            oe = O.OracleEnv(m, env.config_struct, dr=None if dr_table is None else dr_table[i], precision="f64")
         o = oe.step(dict(state=_oracle_record(rec0[i]), obs=obs0[i].astype(np.float64)), a[i].astype(np.float64))
         q_o, v_o = o["state"][0:19], o["state"][19:37]
         dq.append(np.abs(rec1[i, 0:19] - q_o).max())
@@ -115,6 +126,8 @@ def one_step_err(env, n_sample=256, seed=0):
     return {"envs": int(len(ids)), "substeps": int(env._n_frames), "vs": "fp64 oracle restatement, identical start state",
             "qpos_abs": st(dq), "qvel_abs": st(dv), "qpos_rel": st(rq),
             "constraint_flip_envs": int(flagged.sum()),
+            "per_env_model": {"dr": dr_table is not None, "terrain": terrain is not None},
+            "auto_reset_envs_excluded": n_reset,
             "qpos_abs_max_unflagged": float(dq[ok].max()) if ok.any() else None,
             "qvel_abs_max_unflagged": float(dv[ok].max()) if ok.any() else None}
 
@@ -165,8 +178,9 @@ def cpu_baseline(model, cfg, states, obs, seconds_target=12.0):
                       f"not MuJoCo), OpenMP {used} threads, {dt:.1f} s wall"}
 
 
-def qpos_drift(env, nsub=1000):
-    """Standing PD hold: GPU fp32 vs fp64 oracle relative qpos drift after nsub substeps."""
+def qpos_drift(env, nsub=1000, dr_row=None, terrain_row=None):
+    """Standing PD hold: GPU fp32 vs fp64 oracle relative qpos drift after nsub substeps
+    (env 0, against an oracle on env 0's model: its DR row and terrain when the workload has them)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from pupperv3_mjx import _abi, _lib
@@ -186,7 +200,8 @@ def qpos_drift(env, nsub=1000):
     g = env._get(_abi.F_STATE)[0, :19].astype(np.float64)
     q0 = np.zeros(19)
     q0[2], q0[3], q0[7:] = 0.17, 1, dp
-    o, _, _, _, _ = O.mj_step(env.sys_model.struct, q0, np.zeros(18), np.zeros(18), np.array(dp), nsteps=nsub)
+    m = env.sys_model.struct if terrain_row is None else O.model_with_terrain(env.sys_model.struct, terrain_row)
+    o, _, _, _, _ = O.mj_step(m, q0, np.zeros(18), np.zeros(18), np.array(dp), nsteps=nsub, dr=dr_row)
     buf.free()
     return float(np.abs(g - o).max() / np.abs(o).max())
 
@@ -255,16 +270,19 @@ def main():
     E = args.envs
     env = PupperV3Env(**bench_kwargs(model_path, args.random_commands), num_envs=E, device=device, pipeline_output=False)
     L = env._L
+    dr_table, terrain = None, None
     if args.dr:
         from pupperv3_mjx import domain_randomization as dr, rng
         sysb, _ = dr.domain_randomize(env.sys, rng.split(rng.PRNGKey(1000 + rank), E))
         env.set_domain_randomization(sysb)
+        dr_table = sysb.dr_table().astype(np.float64)
     if args.terrain:
         from pupperv3_mjx import obstacles
         if not args.obstacles:
             raise SystemExit("--terrain needs --obstacles N (the box-geom slots)")
-        env.set_terrain(obstacles.sample_terrain(E, args.obstacles, (-5, 5), (-5, 5), height=0.02, length=6.0,
-                                                 seed=args.seed * 1000 + rank, min_boxes=args.obstacles // 2))
+        terrain = obstacles.sample_terrain(E, args.obstacles, (-5, 5), (-5, 5), height=0.02, length=6.0,
+                                           seed=args.seed * 1000 + rank, min_boxes=args.obstacles // 2)
+        env.set_terrain(terrain)
     if args.auto_reset > 0:
         _lib.check(L.pp3_set_auto_reset(env._h, args.auto_reset))
     keys = sharding.shard_keys(args.seed, E * world, world, rank)  # global env ids, contiguous shards
@@ -442,8 +460,10 @@ def main():
                                           "note": "launch time at E / at E/2 envs (one wave per SIMD)"}
         if world == 1 and not args.no_extras:
             out["contact_cap"] = contact_cap_stats(env, acts.ptr.value, min(K, 50))
-            out["one_step_err"] = one_step_err(env)
-            out["qpos_rel_err"] = {"value": qpos_drift(env), "substeps": 1000,
+            out["one_step_err"] = one_step_err(env, dr_table=dr_table, terrain=terrain, auto_reset=args.auto_reset > 0)
+            out["qpos_rel_err"] = {"value": qpos_drift(env, dr_row=None if dr_table is None else dr_table[0],
+                                                       terrain_row=None if terrain is None else terrain[0]),
+                                   "substeps": 1000,
                                    "vs": "fp64 oracle restatement (MuJoCo absent; parity unpinned vs mj_step)",
                                    "trajectory": "standing PD hold"}
             if not args.no_cpu_baseline:

@@ -1,7 +1,8 @@
 """ctypes wrapper of the CPU oracle (TEST INFRASTRUCTURE ONLY).
 
-Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module,
-and only as the checker / CPU baseline -- never as the product path.  See pp3_oracle.c
+Only tests/, __graft_entry__.smoke() and bench.py (its cpu_baseline leg and its untimed
+accuracy checks one_step_err / qpos_rel_err) import this module, and only as the checker /
+CPU baseline -- never as the product path.  See pp3_oracle.c
 for what is restated from where and for the parity status.
 """
 from __future__ import annotations
@@ -73,6 +74,34 @@ def mj_step(model, qpos, qvel, qacc_ws, ctrl, nsteps=1, dr=None, precision="f64"
     L.orc_mj_step(C.byref(model), _p(d), ncon_max, _p(q), _p(v), _p(w), _p(c), nsteps, _p(pipe), _p(sites))
     mj_step.last_boundary = L.orc_boundary_take()
     return q, v, w, pipe, sites
+
+
+GEOM_BOX = 6  # mjGEOM_BOX (pupperv3_mjx._abi.GEOM_BOX)
+
+
+def terrain_slots(model):
+    """cgeom indices of the world box geoms, in slot order (pp3_set_terrain)."""
+    return [g for g in range(model.ncgeom) if model.cgeom_bodyid[g] == 0 and model.cgeom_type[g] == GEOM_BOX]
+
+
+def model_with_terrain(model, rows):
+    """Copy of the model struct whose box geoms hold one env's terrain rows f32[n_boxes, 10]
+    (pos, quat, half-size): the oracle's view of a per-env terrain.  Absent boxes (zero size) are
+    parked below the floor with zero size, as on the device."""
+    m = type(model).from_buffer_copy(model)
+    for b, g in enumerate(terrain_slots(model)):
+        r = np.asarray(rows[b], dtype=np.float64)
+        if not np.any(r[7:10] > 0):
+            pos, quat, size = (0.0, 0.0, -1e4), (1.0, 0.0, 0.0, 0.0), (0.0, 0.0, 0.0)
+        else:
+            q = r[3:7] / np.linalg.norm(r[3:7])
+            pos, quat, size = r[0:3], q, r[7:10]
+        for k in range(3):
+            m.cgeom_pos[g][k] = pos[k]
+            m.cgeom_size[g][k] = size[k]
+        for k in range(4):
+            m.cgeom_quat[g][k] = quat[k]
+    return m
 
 
 def mj_forward(model, qpos, qvel, qacc_ws, ctrl, precision="f64"):

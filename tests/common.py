@@ -159,34 +159,15 @@ def states_with_self_contact(model, jnt_range, n, seed=0, z=0.5, kind="any"):
     return qpos, qvel, np.zeros((n, 18)), qpos[:, 7:].copy()
 
 
-def terrain_slots(model):
-    """cgeom indices of the world box geoms, in slot order (pp3_set_terrain)."""
-    return [g for g in range(model.ncgeom) if model.cgeom_bodyid[g] == 0 and model.cgeom_type[g] == _abi.GEOM_BOX]
+from oracle.oracle import model_with_terrain, terrain_slots  # noqa: E402  (the oracle's terrain view)
+
+assert _abi.GEOM_BOX == 6
 
 
 def model_terrain_rows(model):
     """The model's own static boxes as one terrain row f32[n_boxes, 10]."""
     return np.array([[*model.cgeom_pos[g][:], *model.cgeom_quat[g][:], *model.cgeom_size[g][:]]
                      for g in terrain_slots(model)], dtype=np.float32)
-
-
-def model_with_terrain(model, rows):
-    """Copy of the model struct whose box geoms hold one env's terrain rows (the oracle's view of
-    a per-env terrain; absent boxes are parked below the floor with zero size, as on the device)."""
-    m = type(model).from_buffer_copy(model)
-    for b, g in enumerate(terrain_slots(model)):
-        r = np.asarray(rows[b], dtype=np.float64)
-        if not np.any(r[7:10] > 0):
-            pos, quat, size = (0.0, 0.0, -1e4), (1.0, 0.0, 0.0, 0.0), (0.0, 0.0, 0.0)
-        else:
-            q = r[3:7] / np.linalg.norm(r[3:7])
-            pos, quat, size = r[0:3], q, r[7:10]
-        for k in range(3):
-            m.cgeom_pos[g][k] = pos[k]
-            m.cgeom_size[g][k] = size[k]
-        for k in range(4):
-            m.cgeom_quat[g][k] = quat[k]
-    return m
 
 
 def terrain_under(xy, n_boxes, seed=0, absent_p=0.3):
