@@ -388,7 +388,7 @@ def main():
         launch_s = kernel_ms_max / 1e3 / K
         bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr)
         achieved = bpe * E / launch_s / 1e9
-        traffic, valu, epw, tsrc = None, None, 2, None
+        traffic, valu, epw, tsrc, flops, fsrc = None, None, 2, None, None, None
         if os.path.exists(TRAFFIC_FILE):
             tj = json.load(open(TRAFFIC_FILE))
             if (tj.get("src_sha16") == kernel_source_sha16() and tj.get("envs") == E
@@ -397,6 +397,7 @@ def main():
                 valu = tj.get("valu_insts_per_wave")
                 epw = tj.get("envs_per_wave", 2)
                 tsrc = tj.get("source")
+                flops, fsrc = tj.get("fp32_flops_per_launch"), tj.get("fp32_flops_source")
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -438,6 +439,15 @@ def main():
                                              "ceiling_ms": round(ceil_s * 1e3, 4),
                                              "frac": round(ceil_s / launch_s, 4),
                                              "source": "profiles/traffic_current.json (rocprofv3 SQ_INSTS_VALU)"}
+        if flops:
+            # Arithmetic side: executed FP32 VALU operations per launch from the PMC
+            # instruction mix (64 lanes x (2 FMA + ADD + MUL + TRANS)), over this run's launch time,
+            # against the FP32 vector peak.  Every lane counts, masked or replicated: an upper bound.
+            out["roofline"]["fp32_vector"] = {"executed_flops_per_env_step": round(flops / E, 1),
+                                              "achieved": round(flops / launch_s / 1e12, 3),
+                                              "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                              "frac": round(flops / launch_s / 1e12 / FP32_PEAK_TFLOPS, 5),
+                                              "source": fsrc}
         if (world == 1 and policy is None and not args.gather and E == 4096 and not args.dr and not args.obstacles
                 and not args.auto_reset and not args.no_latency_floor):
             # Latency floor: the same step at E/2 envs puts ONE wave (two envs)
