@@ -27,19 +27,20 @@ NAMES = ["kinematics", "com/cinert/cdof", "limit/friction rows+actuation", "M+bi
 def main():
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     steps = 20
+    warm = int(os.environ.get("DIAG_WARMUP", "5"))  # 5: the driver's window (robots landing); 200: steady state
     env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=False)
     st = env.reset(make_keys(0, E))
     rec = st._record.copy()
     rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]  # bench workload (configs[1])
     env._put(_abi.F_STATE, rec)
     L = env._L
-    acts = _lib.DeviceBuffer((steps + 5) * E * 48)
-    _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, (steps + 5) * E * 12, 1, 0, -1.0, 1.0, None))
+    acts = _lib.DeviceBuffer((steps + warm) * E * 48)
+    _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, (steps + warm) * E * 12, 1, 0, -1.0, 1.0, None))
     ms = C.c_float()
-    _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, 5, C.byref(ms)))
+    _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, warm, C.byref(ms)))
     buf = (C.c_uint64 * 22)()
     _lib.check(L.pp3_phase_profile(buf, 22, 1))
-    _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + 5 * E * 48), E * 12, steps, C.byref(ms)))
+    _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + warm * E * 48), E * 12, steps, C.byref(ms)))
     _lib.check(L.pp3_phase_profile(buf, 22, 1))
     v = np.array(buf[:len(NAMES)], dtype=np.float64)
     tot = v.sum()
