@@ -1,7 +1,8 @@
 """The kernel at the headline launch geometries of BASELINE.json (not just 1-64 envs).
 
 configs[1]: 4096 envs (2048 one-wave workgroups: every CU holds a full generation), flat,
-fixed command (0.5, 0, 0), no DR.  configs[3] per GPU: 8192 envs (two generations), commands
+fixed command (0.5, 0, 0), no DR; the same with domain randomisation (configs[2]) and with the 10
+obstacle boxes (configs[4] per GPU).  configs[3] per GPU: 8192 envs (two generations), commands
 sampled at reset and resampled every 500 steps.  Plus an odd batch (4097: the last wave's
 second half recomputes env N-1 and must store nothing).  configs[0] (1 env, zero command,
 mj_step plumbing) runs as C1 below: 1000 free-running env steps against the fp64 oracle.
@@ -31,9 +32,15 @@ def _sample_ids(n, k=64, seed=0):
     return sorted(ids)
 
 
-def _run(require_gpu, n, random_commands, name):
-    env = PupperV3Env(**bench_kwargs(MODEL_XML, random_commands), num_envs=n)
+def _run(require_gpu, n, random_commands, name, model_path=MODEL_XML, dr=False):
+    env = PupperV3Env(**bench_kwargs(model_path, random_commands), num_envs=n)
     try:
+        table = None
+        if dr:  # configs[2]: a domain-randomised model per env (domain_randomization.py:11-18 ranges)
+            from pupperv3_mjx import domain_randomization, rng
+            sysb, _ = domain_randomization.domain_randomize(env.sys, rng.split(rng.PRNGKey(1000), n))
+            env.set_domain_randomization(sysb)
+            table = sysb.dr_table().astype(np.float64)
         keys = make_keys(7, n)
         st = env.reset(keys)
         if not random_commands:
@@ -59,11 +66,13 @@ def _run(require_gpu, n, random_commands, name):
         a = rs.uniform(-1, 1, size=(n, 12)).astype(np.float32)
         prev = st
         st = env.step(prev, a)
-        oe = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f32")
+        base = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f32")
         scales = np.array(env.config_struct.reward_scales[:])
         fb = G.FlipBudget(max_frac=0.02, name=name)
         stats = G.TermStats()
         for i in _sample_ids(n):
+            oe = base if table is None else O.OracleEnv(env.sys_model.struct, env.config_struct, dr=table[i],
+                                                         precision="f32")
             o = oe.step(dict(state=G.record_to_oracle_state(prev._record[i]), obs=prev.obs[i].astype(np.float64)),
                         a[i].astype(np.float64))
             orec = G.oracle_state_to_record(o["state"])
@@ -92,6 +101,21 @@ def test_configs1_4096_envs(require_gpu):
 
 def test_configs3_8192_envs_random_commands(require_gpu):
     _run(require_gpu, 8192, True, "headline_8192")
+
+
+def test_configs2_4096_envs_domain_randomised(require_gpu):
+    _run(require_gpu, 4096, False, "headline_4096_dr", dr=True)
+
+
+def test_configs4_4096_envs_obstacle_boxes(require_gpu, tmp_path):
+    """configs[4] per GPU: the 10 obstacles.py boxes of the golden layout (seed 0) in the model."""
+    import xml.etree.ElementTree as ET
+    from pupperv3_mjx import obstacles
+    tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
+    obstacles.add_boxes_to_model(tree, n_boxes=10, x_range=(-5, 5), y_range=(-5, 5), height=0.02, length=6.0)
+    path = str(tmp_path / "pupper_obstacles.xml")
+    tree.write(path, encoding="unicode")
+    _run(require_gpu, 4096, False, "headline_4096_obstacles", model_path=path)
 
 
 def test_odd_batch_4097_envs(require_gpu):

@@ -3,6 +3,9 @@
 # per-launch time over the first 300 steps after reset (regular build)
 OUT=gpurun_out/s4f
 mkdir -p $OUT
+export PP3_REPORT_DIR=$OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_headline.py -x -v --timeout 200 --timeout-method thread > $OUT/headline_tests.log 2>&1; rc=$?; echo headline_rc=$rc; grep -E "PASS|FAIL|Error" $OUT/headline_tests.log | tail -8
+[ $rc -eq 0 ] || exit 1
 PP3_DIAG_OUT=$OUT DIAG_WARMUP=5 timeout -k 10 200 python3 tests/diag_phases.py > $OUT/phases_w5.txt 2>&1 || exit 1
 PP3_DIAG_OUT=$OUT DIAG_WARMUP=200 timeout -k 10 200 python3 tests/diag_phases.py > $OUT/phases_w200.txt 2>&1 || exit 1
 timeout -k 10 200 python3 - > $OUT/launch_curve.txt 2>&1 <<'PY' || exit 1
