@@ -66,3 +66,32 @@ def test_allreduce_and_barrier(comm):
     np.testing.assert_array_equal(comm.allreduce([1.5, -2.0], "sum"), [1.5, -2.0])
     comm.barrier()
     assert comm._L.pp3_comm_world(comm._h) == 1 and comm._L.pp3_comm_rank(comm._h) == 0
+
+
+def test_gather_at_configs3_shard_size(comm):
+    """configs[3]'s per-GPU shard (8192 envs, random commands) after steps: the hand-over rows of
+    every env equal the env's own obs | reward | done, bit for bit (pack + RCCL on the env stream,
+    no host synchronisation between the step and the gather)."""
+    from bench import bench_kwargs
+    n = 8192
+    env = PupperV3Env(**bench_kwargs(common.MODEL_XML, True), num_envs=n, pipeline_output=False)
+    try:
+        env.reset(make_keys(5, n))
+        width = env.observation_size + 2
+        dst = _lib.DeviceBuffer(n * width * 4, env.device)
+        acts = _lib.DeviceBuffer(n * 12 * 4, env.device)
+        rs = np.random.RandomState(2)
+        for _ in range(3):
+            env.synchronize()  # the previous step has consumed the action buffer
+            acts.upload(rs.uniform(-1, 1, size=(n, 12)).astype(np.float32))
+            env.step_device(acts.ptr.value)
+            comm.gather(env, n, dst.ptr.value, root=0)
+        env.synchronize()
+        got = np.empty((n, width), np.float32)
+        dst.download(got)
+        obs, rew, done = env._get(_abi.F_OBS), env._get(_abi.F_REWARD), env._get(_abi.F_DONE)
+        np.testing.assert_array_equal(got, sharding.pack_rows(obs, rew.reshape(n), done.reshape(n), n))
+        dst.free()
+        acts.free()
+    finally:
+        env.close()
