@@ -11,14 +11,21 @@ data-path collective (weak scaling); barrier + max-over-ranks timing over RCCL.
 
   python bench.py [--gpus N --steps K --warmup W --envs E --dr --gather --no-cpu-baseline]
 
-No torch: multi-GPU ranks (RANK / WORLD_SIZE / LOCAL_RANK from torch.distributed.run or any
-launcher) talk through the library's own RCCL communicator (pp3_comm_*: barrier, max-over-ranks
-timing, the --gather collective), created from an id exchanged by a file rendezvous on the node.
+Multi-GPU: `python bench.py --gpus N` starts N rank processes itself (launch_ranks: RANK /
+LOCAL_RANK / WORLD_SIZE set per child, before this process touches HIP) and relays rank 0's JSON
+line; under torch.distributed.run (WORLD_SIZE already set) the process is one rank and --gpus
+must equal WORLD_SIZE.  No torch: ranks talk through the library's own RCCL communicator
+(pp3_comm_*: barrier, max-over-ranks timing, the --gather collective), created from an id
+exchanged by a file rendezvous on the node.  With N > 1 every run also checks the multi-rank
+gather once, untimed (gather_check: per-rank checksums of the packed rows vs what landed at the
+root and in the all-gather).
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -206,9 +213,87 @@ def qpos_drift(env, nsub=1000, dr_row=None, terrain_row=None):
     return float(np.abs(g - o).max() / np.abs(o).max())
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (this script, RANK / LOCAL_RANK /
+    WORLD_SIZE set, one GPU each), wait for them and return the job's exit status (rank 0 prints
+    the JSON line; its stdout is this process's).  This parent never touches HIP or the GPU and
+    never execs: it only spawns children.  If one rank fails, the others are stopped (they would
+    otherwise wait in the next barrier) and the job fails."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    nonce = f"bench{os.getpid()}.{time.time_ns()}"
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PP3_LAUNCH_ID=nonce)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.remove(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py launcher: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def gather_check(env, comm, world, rank, nmax):
+    """Untimed check of the multi-rank hand-over (pp3_gather), run once per N > 1 job: each rank's
+    checksum of its OWN packed rows (sharding.pack_rows of its obs / reward / done), all-reduced,
+    must equal the checksum of rank r's slot of what arrived at the root (root 0, grouped send /
+    recv) and at every rank (root -1, all-gather); each receiver's own slot must equal its rows bit
+    for bit.  Returns the report; every rank learns the verdict (one all-reduce)."""
+    import numpy as np
+    from pupperv3_mjx import _abi, _lib, sharding
+    env.synchronize()
+    mine = sharding.pack_rows(env._get(_abi.F_OBS), env._get(_abi.F_REWARD), env._get(_abi.F_DONE), nmax)
+    W = mine.shape[1]
+    wts = 1.0 + (np.arange(mine.size, dtype=np.float64) % 1021) / 1021.0  # position-sensitive
+
+    def csum(rows):
+        return float(np.dot(rows.astype(np.float64).ravel(), wts))
+    vec = np.zeros(world)
+    vec[rank] = csum(mine)
+    expect = comm.allreduce(vec, "sum")  # one nonzero term per entry: exact
+    dst = _lib.DeviceBuffer(world * nmax * W * 4, env.device)
+    bad = 0
+    report = {}
+    for root in (0, -1):
+        recv = root < 0 or rank == root
+        comm.gather(env, nmax, dst.ptr.value if recv else None, root=root)
+        env.synchronize()
+        if recv:
+            full = np.empty((world * nmax, W), dtype=np.float32)
+            dst.download(full)
+            got = [csum(full[r * nmax:(r + 1) * nmax]) for r in range(world)]
+            ok = all(g == e for g, e in zip(got, expect)) and np.array_equal(full[rank * nmax:(rank + 1) * nmax], mine)
+            bad += 0 if ok else 1
+            if rank == 0:
+                report["root0" if root == 0 else "allgather"] = "ok" if ok else "MISMATCH"
+    dst.free()
+    nbad = int(comm.allreduce([float(bad)], "sum")[0])
+    report.update(ranks=world, rows_per_rank=nmax, row_floats=W, failing_receivers=nbad,
+                  check="per-rank float64 checksums of pack_rows vs the received slots")
+    return report
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of the job; default WORLD_SIZE under a launcher, else 1")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="ranks report RANK / LOCAL_RANK / WORLD_SIZE as a JSON line and exit before any HIP call")
+    ap.add_argument("--no-gather-check", action="store_true", help="skip the N > 1 gather_check")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=200,
                     help="untimed steps first: the drop from the start height settles (steady state)")
@@ -235,9 +320,17 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus))  # this process only spawns the ranks (no HIP here)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.dry_launch:
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world, "pid": os.getpid(),
+                          "launch": os.environ.get("PP3_LAUNCH_ID")}), flush=True)
+        return
     # rehearsal knob for the multi-rank code on one GPU (never used by the driver): every rank on
     # this device
     device = int(os.environ.get("PP3_BENCH_DEVICE", local_rank))
@@ -376,6 +469,15 @@ def main():
         wall_max, kernel_ms_max = (float(v) for v in comm.allreduce([wall, kernel_ms], "max"))
     else:
         wall_max, kernel_ms_max = wall, kernel_ms
+    n_gpus = comm.world if comm is not None else 1  # the ranks that actually joined the job
+    gcheck = None
+    if world > 1 and not args.no_gather_check:
+        if isinstance(comm, sharding.Comm):
+            gcheck = gather_check(env, comm, world, rank, E)
+            if gcheck["failing_receivers"]:
+                print(f"rank {rank}: gather_check failed: {gcheck}", file=sys.stderr, flush=True)
+        else:
+            gcheck = {"skipped": f"no RCCL communicator ({comm_kind})"}
 
     # sanity on the produced batch
     rew = env._get(_abi.F_REWARD)
@@ -402,7 +504,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "env-steps/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max / K * 1e3, 4),
@@ -421,7 +523,7 @@ def main():
                        if not args.gather else f"env-sharded x{world} + per-step RCCL gather to rank {args.gather_root}",
                        "per_env_terrain": bool(args.terrain),
                        "commands": "reset-sampled, resampled every 500 steps" if args.random_commands else "fixed (0.5,0,0)",
-                       "gather": gather_info, "comm": comm_kind, "auto_reset_episode_length": args.auto_reset or None,
+                       "gather": gather_info, "gather_check": gcheck, "comm": comm_kind, "auto_reset_episode_length": args.auto_reset or None,
                        "policy_in_loop": args.policy or None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
@@ -486,6 +588,8 @@ def main():
     env.close()
     if comm is not None:
         comm.close()
+    if gcheck and gcheck.get("failing_receivers"):
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -334,6 +334,8 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg,
 int pp3_destroy(pp3_env_t* env);
 int32_t pp3_num_envs(const pp3_env_t* env);
 int32_t pp3_state_stride(const pp3_env_t* env);
+/* The HIP device the handle was created on (-1 for NULL). */
+int32_t pp3_env_device(const pp3_env_t* env);
 
 /* reset(rng): keys_dev = uint32[N][2] (one jax PRNG key per env); mask_dev =
  * optional uint8[N] (NULL = all envs).  environment.py:314-346. */
@@ -484,7 +486,9 @@ const char* pp3_comm_last_error(void);
  * count; rows past the count are zero) of width 36H + 2 = [obs | reward | done], rank r's rows
  * at dst_dev + r * nmax * (36H + 2).  root >= 0: gather to rank `root` (grouped send/recv,
  * dst_dev needed on the root only); root < 0: all-gather (dst_dev on every rank).  Enqueued on
- * `stream` (NULL = the env's stream): ordered after the env's last step, no host sync. */
+ * `stream` (NULL = the env's stream): ordered after the env's last step, no host sync.  The env
+ * must live on the communicator's device (PP3_ERR_ARG otherwise); the caller's current HIP device
+ * is restored on return. */
 int pp3_gather(pp3_comm_t* comm, pp3_env_t* env, int32_t nmax, int32_t root, float* dst_dev, void* stream);
 /* Host-blocking helpers for timing: element-wise sum / max of n <= 64 doubles over ranks, and
  * a barrier. */

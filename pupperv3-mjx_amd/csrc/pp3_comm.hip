@@ -20,6 +20,7 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 
 #include "pupper_hip.h"
@@ -46,24 +47,25 @@ int cerr(int code, const std::string& m) {
   return code;
 }
 
-const Rccl* rccl() {
-  static Rccl r;
-  static bool tried = false;
-  if (tried) return r.so ? &r : nullptr;
-  tried = true;
+// loaded once per process (std::call_once: safe from several host threads); a failure is
+// remembered and reported to every caller
+Rccl g_rccl;
+std::string g_rccl_err;
+void load_rccl() {
+  Rccl& r = g_rccl;
   const char* names[] = {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
   for (const char* n : names)
     if ((r.so = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
   if (!r.so) {
-    g_cerr = std::string("cannot load librccl.so.1: ") + dlerror();
-    return nullptr;
+    g_rccl_err = std::string("cannot load librccl.so.1: ") + dlerror();
+    return;
   }
 #define SYM(field, name)                                                          \
   r.field = reinterpret_cast<decltype(r.field)>(dlsym(r.so, name));               \
   if (!r.field) {                                                                 \
-    g_cerr = std::string("librccl.so.1 lacks ") + name;                           \
+    g_rccl_err = std::string("librccl.so.1 lacks ") + name;                       \
     r.so = nullptr;                                                               \
-    return nullptr;                                                               \
+    return;                                                                       \
   }
   SYM(GetUniqueId, "ncclGetUniqueId")
   SYM(CommInitRank, "ncclCommInitRank")
@@ -76,8 +78,29 @@ const Rccl* rccl() {
   SYM(GroupEnd, "ncclGroupEnd")
   SYM(GetErrorString, "ncclGetErrorString")
 #undef SYM
-  return &r;
 }
+const Rccl* rccl() {
+  static std::once_flag once;
+  std::call_once(once, load_rccl);
+  if (!g_rccl.so) {
+    g_cerr = g_rccl_err;
+    return nullptr;
+  }
+  return &g_rccl;
+}
+
+// sets `device` current for the scope and restores the caller's device on exit
+struct DeviceScope {
+  int prev = -1;
+  hipError_t err;
+  explicit DeviceScope(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = hipSetDevice(device);
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 #define HCHK(x)                                                                                   \
   do {                                                                                            \
@@ -133,7 +156,8 @@ int pp3_comm_init(const uint8_t* id, int32_t rank, int32_t world, int32_t device
   if (!id || !out || world < 1 || rank < 0 || rank >= world) return cerr(PP3_ERR_ARG, "pp3_comm_init: bad argument");
   const Rccl* R = rccl();
   if (!R) return cerr(PP3_ERR_COMM, g_cerr);
-  HCHK(hipSetDevice(device));
+  DeviceScope dev(device);
+  HCHK(dev.err);
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
   pp3_comm* c = new pp3_comm();
@@ -149,6 +173,7 @@ int pp3_comm_init(const uint8_t* id, int32_t rank, int32_t world, int32_t device
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->red, 64 * sizeof(double)) != hipSuccess) {
     R->CommDestroy(c->comm);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return cerr(PP3_ERR_HIP, "pp3_comm_init: stream / scratch allocation failed");
   }
@@ -159,7 +184,7 @@ int pp3_comm_init(const uint8_t* id, int32_t rank, int32_t world, int32_t device
 int pp3_comm_destroy(pp3_comm_t* c) {
   if (!c) return PP3_OK;
   const Rccl* R = rccl();
-  (void)hipSetDevice(c->device);
+  DeviceScope dev(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (R) R->CommDestroy(c->comm);
   (void)hipFree(c->pack);
@@ -175,6 +200,8 @@ int32_t pp3_comm_world(const pp3_comm_t* c) { return c ? c->world : 0; }
 int pp3_gather(pp3_comm_t* c, pp3_env_t* e, int32_t nmax, int32_t root, float* dst_dev, void* stream) {
   if (!c || !e) return cerr(PP3_ERR_ARG, "pp3_gather: null argument");
   if (root >= c->world) return cerr(PP3_ERR_ARG, "pp3_gather: root out of range");
+  if (pp3_env_device(e) != c->device)
+    return cerr(PP3_ERR_ARG, "pp3_gather: the env and the communicator are on different devices");
   const int n = pp3_num_envs(e);
   if (nmax < n) return cerr(PP3_ERR_ARG, "pp3_gather: nmax smaller than this rank's shard");
   if ((root < 0 || root == c->rank) && !dst_dev) return cerr(PP3_ERR_ARG, "pp3_gather: null destination");
@@ -187,7 +214,8 @@ int pp3_gather(pp3_comm_t* c, pp3_env_t* e, int32_t nmax, int32_t root, float* d
     return cerr(PP3_ERR_ARG, std::string("pp3_gather: ") + pp3_last_error());
   const size_t W = (size_t)D + 2, count = (size_t)nmax * W;
   hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)pp3_stream(e);
-  HCHK(hipSetDevice(c->device));
+  DeviceScope dev(c->device);
+  HCHK(dev.err);
   // the root packs straight into its own slot of the destination; every other chunk is staged
   float* mine;
   if (root >= 0 && root == c->rank) {
@@ -229,7 +257,8 @@ int pp3_comm_allreduce(pp3_comm_t* c, const double* in, double* out, int32_t n, 
   if (!c || !in || !out || n < 1 || n > 64) return cerr(PP3_ERR_ARG, "pp3_comm_allreduce: bad argument (n <= 64)");
   const Rccl* R = rccl();
   if (!R) return cerr(PP3_ERR_COMM, g_cerr);
-  HCHK(hipSetDevice(c->device));
+  DeviceScope dev(c->device);
+  HCHK(dev.err);
   HCHK(hipMemcpyAsync(c->red, in, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
   NCHK(R, R->AllReduce(c->red, c->red, n, ncclFloat64, op == PP3_REDUCE_MAX ? ncclMax : ncclSum, c->comm, c->stream));
   HCHK(hipMemcpyAsync(out, c->red, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "pp3_device.h"
+#include "pp3_diag.h"
 
 namespace pp3 {
 
@@ -142,55 +143,6 @@ __device__ __forceinline__ LaneRec<N> fetch_rec(const LaneTab<N>& t, int l) {
 }
 __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 
-// Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-cycle deltas summed over all
-// waves.  A stamp is one s_memtime (its lgkmcnt wait drains the LDS reads in flight) and two VALU:
-// lane k of a per-wave register accumulates phase k's cycles, one global atomic per lane at the
-// end of the launch (gfx950 has no SHADER_CYCLES hwreg).
-#ifdef PP3_PHASE_PROF
-constexpr int NPROF = 22;  // 0..18 phase cycles, 19 line-search evaluations per wave (max of its two envs), 20 per env
-struct Prof {
-  uint32_t t, acc;
-  uint32_t t0, dense, ncmax, evals;  // per wave: start stamp, dense-Hessian substeps, max contacts, line-search evaluations
-  uint32_t csum, slot2;               // contacts summed over substeps (max of the two envs), substeps using row slot 1
-  uint32_t n, tr0, tr1, k0, k1;       // stamp trace: stamp i held by lane i % 64 in tr{i / 64}, its phase in k{i / 64}
-};
-constexpr int MAXWAVE = 16384;
-constexpr int NTRACE = 128;
-constexpr int WREC = 32 + 2 * NTRACE;  // + the stamp trace (stamps, then phase ids; 0xffffffff = unused)
-__device__ uint32_t g_wave[MAXWAVE][WREC];  // last launch: lifetime cycles, dense substeps, max ncon, evaluations,
-                                            // start stamp, end stamp, HW_ID, XCC_ID, 8..26 the wave's cycles
-                                            // per phase, 27 csum, 28 slot2, 29/30 s_memrealtime at start/end
-// per-wave slots summed on the host: no contended device-scope atomics at wave exit (45 k atomics
-// on 22 addresses clogged the memory path that the remaining waves' scalar loads share, and
-// stalled them by 20-80 k cycles: tools/wave_trace.py)
-__device__ unsigned long long g_prof[MAXWAVE][NPROF];
-__device__ __forceinline__ uint32_t shader_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
-#define PROF_PARAM , Prof* pf
-#define PROF_ARG , pf
-#define PROF_NULL , (Prof*)nullptr
-#define PROF_ADD(k, v) do { if (pf) pf->acc += ((int)(threadIdx.x) == (k)) ? (uint32_t)(v) : 0u; } while (0)
-#define PHASE(k)                                                            \
-  do {                                                                      \
-    if (pf) {                                                               \
-      asm volatile("; PP3PHASE " #k);                                       \
-      const uint32_t t_ = shader_cycles();                                  \
-      pf->acc += ((int)(threadIdx.x) == (k)) ? (t_ - pf->t) : 0u;         \
-      pf->t = t_;                                                           \
-      const uint32_t i_ = pf->n++;                                          \
-      if ((i_ & 63u) == (threadIdx.x & 63u)) {                              \
-        if (i_ < 64u) { pf->tr0 = t_; pf->k0 = (k); }                        \
-        else if (i_ < 128u) { pf->tr1 = t_; pf->k1 = (k); }                  \
-      }                                                                     \
-    }                                                                       \
-  } while (0)
-#else
-#define PROF_PARAM
-#define PROF_ARG
-#define PROF_NULL
-#define PROF_ADD(k, v) do { } while (0)
-#define PHASE(k) do { } while (0)
-#endif
-
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // wave priority by load (env_step_kernel): contact-weight thresholds (contacts of the busier env
@@ -200,10 +152,6 @@ __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x)
 #endif
 #ifndef PP3_HEAVY2
 #define PP3_HEAVY2 100
-#endif
-
-#ifdef PP3_DEBUG
-__device__ float g_dbg[512];  // last Newton iteration of env 0 (debug build only)
 #endif
 
 // ---------------------------- half-wave primitives ----------------------------
@@ -1312,12 +1260,6 @@ template <int NC>
 __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
   l = opaque_lane(l);
-  // timing ablation only (-DPP3_AB_DUP=k, tools/ab_build.sh): phase k runs twice (the phases so
-  // marked are idempotent), its cost = the time delta
-#ifndef PP3_AB_DUP
-#define PP3_AB_DUP 0
-#endif
-#define AB_REP(k) for (int ab_r_ = 0; ab_r_ < (PP3_AB_DUP == (k) ? 2 : 1); ab_r_++)
   // the com and M-entry phases' lane records, loaded here without a wait: they arrive while
   // kinematics runs (a pinned fetch at the phase itself costs a round trip there)
   LaneRec<2> rc_pf;
@@ -1339,13 +1281,13 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
   kinematics(s, m, l, integrate_prev); SYNC();
   PHASE(0); l = opaque_lane(l);
-  AB_REP(2) { com_pos(s, m, l, h, rc_pf); SYNC(); }
+  { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
-  AB_REP(3) { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
+  { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
   int lsup = 4;  // lane c: support of contact c (4 = none)
-  AB_REP(4) { lsup = collision(s, m, l, h, pair_pf); SYNC(); }
+  { lsup = collision(s, m, l, h, pair_pf); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   // the PairCon of contact c = l / 4 for the first batch of phase 13's edge rows (lane e = 4c + k),
   // loaded here unpinned: it arrives during the limit/actuation and M-entry phases
@@ -1411,7 +1353,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   PHASE(2); l = opaque_lane(l);
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
   const LaneRec<3> rm = rm_pf;  // (prefetched at the substep start; also read by phases 13 and 7)
-  AB_REP(5)
+  
 #pragma unroll
   for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count
     const int ij = as_i(rm.f[LM_IJ + t]);
@@ -1455,7 +1397,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   SYNC();
   PHASE(3); l = opaque_lane(l);
   // ---- phase 5: qfrc_bias/smooth (subtree sums of body forces), contact edge rows ----
-  AB_REP(12) {
+  {
   if (l < NV) {
     float cf[6];
     if (l < 6) {
@@ -1477,7 +1419,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     for (int k = 0; k < 6; k++) bias += s.cdof[l][k] * cf[k];
     s.qfrc_smooth[l] = -rm.f[LM_DAMP] * s.qvel[l] - bias + s.qfrc_act[l];
   }
-  }  // AB_REP(12): the bias part only
+  }
   const int nl = s.nl;
   __builtin_assume(nl >= 0 && nl <= NLMAX);
   const int nefc = NFR + nl + 4 * ncon;
@@ -1508,16 +1450,12 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   PHASE(13); l = opaque_lane(l);
   // ---- phase 6: qacc_smooth = M^-1 qfrc_smooth (register LDL) ----
   float mrow[NV];  // this lane's permuted row of M, kept for the Newton Hessian (no second load)
-  AB_REP(6) {
+  {
     const int lp = l < NV ? l : NV - 1, dn = pnat(lp);  // permuted row held by this lane
     float a[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) { a[j] = s.M[dn][pnat(j)]; mrow[j] = a[j]; }
-#ifdef PP3_AB_NO_LDLM  // timing ablation only: diagonal solve
-    const float x = s.qfrc_smooth[dn] / a[lp];
-#else
     const float x = ldl_arrow_solve(a, s.qfrc_smooth[dn], l, &s.x.L[0][0]);
-#endif
     if (l < NV) s.qacc_smooth[dn] = x;
   }
   SYNC();
@@ -1543,7 +1481,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   float cws = 0, csm = 0;
   float xws[NR], xsm[NR], ma_ws = 0.0f;
   bool use_smooth;
-  AB_REP(8) {
+  {
 #pragma unroll
     for (int t = 0; t < NR; t++) {
       xws[t] = 0.0f;
@@ -1645,12 +1583,8 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     // Hessian rows H = M + J' D J (registers), LDL^T, search = -H^-1 grad.  Contacts that
     // touch one leg (+ base) keep H arrowhead -> tree-sparse LDL in permuted order; a contact
     // coupling two legs (either env of the wave) switches the wave to the dense factorisation.
-    AB_REP(10) {
-#ifdef PP3_AB_NO_DENSE  // timing ablation only: the arrowhead solve even with leg-leg contacts (wrong physics)
-      const bool dense = false;
-#else
+    {
       const bool dense = __ballot((lsup & 7) == 5) != 0;  // a leg-leg contact in either env
-#endif
       weight = cmax + (dense ? 2 : 0);
 #ifdef PP3_PHASE_PROF
       if (pf) {
@@ -1684,11 +1618,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
           }
         }
         PHASE(14); l = opaque_lane(l);
-#ifdef PP3_AB_NO_LDLH  // timing ablation only: diagonal solve
-        const float x = s.grad[dn] / a[lp];
-#else
         const float x = ldl_arrow_solve(a, s.grad[dn], l, &s.x.L[0][0]);
-#endif
         if (l < NV) s.search[dn] = -x;
       } else {
         dense_search<NC>((LdsShared<NC>*)&s, l, h, cmax, ncon, lsup);
@@ -1763,12 +1693,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     // below is per env (per half), the wave runs the union of both envs' evaluations
     float alpha = 0.0f;
     int evals = 0;
-#ifdef PP3_AB_NO_LS  // timing ablation only: full Newton step
-    alpha = live ? 1.0f : 0.0f;
-    if (false) {
-#else
     if (live) {
-#endif
       const int maxit = m.ls_iterations;
       float c0, g0, h0;
       eval(0.0f, c0, g0, h0);
@@ -2289,9 +2214,6 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   SYNC();
   PHASE(10);
   // ---- physics: n_frames x mj_step (environment.py:366) ----
-#ifdef PP3_AB_FRAMES
-  n_frames = PP3_AB_FRAMES;  // timing ablation only
-#endif
   asm volatile("" : "+s"(n_frames));  // one scalar load (an invariant load is otherwise re-issued per substep)
   // VALU issue between the two waves of a SIMD goes by priority, then age: at equal priority the
   // younger wave (wave slot 1 in 97 % of pairs) only gets the older one's leftover issue cycles
@@ -2327,11 +2249,6 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   else if (wslot) __builtin_amdgcn_s_setprio(1);
   else __builtin_amdgcn_s_setprio(0);
   SYNC();
-#ifdef PP3_AB_NO_EPILOGUE  // timing ablation only (tools/ab_build.sh): state out, no obs/reward
-  if (own)
-    for (int t = l; t < PP3_S_ACT_BUF; t += HW) gst[t] = s.qpos[t % 20] + s.qvel[t % 18];
-  return;
-#endif
   // The epilogue reads the model through a fresh opaque constant-AS pointer: after the loop's
   // asm'd pointer, reads through the kernel-level reference are no longer proven uniform and
   // turn into per-use vector loads (one vmcnt round trip each) instead of s_load.
@@ -3190,6 +3107,12 @@ static int alloc_env_buffers(pp3_env* e, const DevModel& hm);
 
 int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t num_envs, int32_t device, pp3_env_t** out) {
   if (!model || !cfg || !out || num_envs < 1) return set_err(PP3_ERR_ARG, "bad arguments to pp3_create");
+  if (PP3_DIAG_BUILD) {  // pp3_diag.h: a diagnostic library is never the product
+    const char* ok = getenv("PP3_ALLOW_DIAG_BUILD");
+    if (!ok || strcmp(ok, "1") != 0)
+      return set_err(PP3_ERR_ARG, "pp3_create: this library is a diagnostic build (PP3_PHASE_PROF / PP3_DEBUG); "
+                                  "set PP3_ALLOW_DIAG_BUILD=1 to use it for diagnostics");
+  }
   DevModel hm;
   int rc = build_devmodel(model, cfg, &hm);
   if (rc) return rc;
@@ -3259,6 +3182,7 @@ int pp3_destroy(pp3_env_t* e) {
 
 int32_t pp3_num_envs(const pp3_env_t* e) { return e ? e->N : 0; }
 int32_t pp3_state_stride(const pp3_env_t* e) { return e ? e->stride : 0; }
+int32_t pp3_env_device(const pp3_env_t* e) { return e ? e->device : -1; }
 
 static hipStream_t stream_of(pp3_env_t* e, void* s) { return s ? (hipStream_t)s : e->stream; }
 

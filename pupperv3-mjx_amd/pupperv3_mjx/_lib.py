@@ -40,6 +40,8 @@ def load() -> C.CDLL:
     L.pp3_num_envs.restype = i32
     L.pp3_state_stride.argtypes = [vp]
     L.pp3_state_stride.restype = i32
+    L.pp3_env_device.argtypes = [vp]
+    L.pp3_env_device.restype = i32
     L.pp3_reset.argtypes = [vp, vp, vp, vp]
     L.pp3_step.argtypes = [vp, vp, vp]
     L.pp3_set_dr.argtypes = [vp, vp]
@@ -114,8 +116,8 @@ def check_comm(rc: int) -> None:
 
 EXPORTED_SYMBOLS = (
     "pp3_abi_version", "pp3_struct_size", "pp3_last_error", "pp3_device_count", "pp3_create", "pp3_destroy",
-    "pp3_num_envs", "pp3_state_stride", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
-    "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
+    "pp3_num_envs", "pp3_state_stride", "pp3_env_device", "pp3_reset", "pp3_step", "pp3_set_dr",
+    "pp3_set_pipeline_output", "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
     "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",

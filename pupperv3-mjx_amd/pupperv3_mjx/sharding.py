@@ -74,17 +74,38 @@ def unpack_gathered(full, global_envs: int, world: int):
 _RDZV_ERR = b"PP3_RDZV_ERROR:"  # (an id is COMM_ID_BYTES of binary; this prefix marks rank 0's failure)
 
 
+def _proc_start_ticks(pid: int) -> str:
+    """Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), or "0"."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[19]
+    except (OSError, IndexError):
+        return "0"
+
+
+def launch_key() -> str:
+    """A value every rank of ONE launch shares and no other launch does.  bench.py's own launcher
+    exports PP3_LAUNCH_ID (a per-launch nonce); under torch.distributed.run every worker of a launch
+    has the same parent (the elastic agent): its pid together with its start time (pids are reused,
+    pid + start time are not), MASTER_PORT and TORCHELASTIC_RUN_ID key the launch."""
+    explicit = os.environ.get("PP3_LAUNCH_ID")
+    if explicit:
+        return explicit
+    ppid = os.getppid()
+    port = os.environ.get("MASTER_PORT", "0")
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "none")
+    return f"{ppid}.{_proc_start_ticks(ppid)}_{port}_{run}"
+
+
 def _rdzv_path(tag: str) -> str:
-    """Per-launch file name on the node.  Explicit PP3_RDZV_FILE wins (e.g. a shared file system
-    for several nodes); under torch.distributed.run every worker of one launch has the same
-    parent (the elastic agent) and MASTER_PORT, which key the file."""
+    """Per-launch file name on the node (launch_key): a file left behind by an earlier launch can
+    never be read by a later one.  Explicit PP3_RDZV_FILE wins (e.g. a shared file system for
+    several nodes)."""
     explicit = os.environ.get("PP3_RDZV_FILE")
     if explicit:
         return explicit + tag
     base = os.environ.get("PP3_RDZV_DIR", "/tmp")
-    port = os.environ.get("MASTER_PORT", "0")
-    run = os.environ.get("TORCHELASTIC_RUN_ID", "none")
-    return os.path.join(base, f"pp3_rdzv_{os.getppid()}_{port}_{run}{tag}.bin")
+    return os.path.join(base, f"pp3_rdzv_{launch_key()}{tag}.bin")
 
 
 def rendezvous_id(rank: int, world: int, make_id: Callable[[], bytes], tag: str = "",
@@ -146,15 +167,18 @@ class Comm:
             _lib.check_comm(L.pp3_comm_unique_id(buf))
             return bytes(buf)
 
-        uid = rendezvous_id(self.rank, self.world, make_id, tag)
-        ubuf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
-        h = C.c_void_p()
-        _lib.check_comm(L.pp3_comm_init(ubuf, self.rank, self.world, self.device, C.byref(h)))
-        self._h = h
-        self._tag = tag
-        self.barrier()  # every rank has read the id: rank 0 may remove the file
-        if self.rank == 0:
-            rendezvous_cleanup(tag)
+        self._h = None
+        try:
+            uid = rendezvous_id(self.rank, self.world, make_id, tag)
+            ubuf = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+            h = C.c_void_p()
+            _lib.check_comm(L.pp3_comm_init(ubuf, self.rank, self.world, self.device, C.byref(h)))
+            self._h = h
+            self._tag = tag
+            self.barrier()  # every rank has read the id: rank 0 may remove the file
+        finally:
+            if self.rank == 0:  # (also when the init failed: no later launch may find it)
+                rendezvous_cleanup(tag)
 
     @classmethod
     def from_env(cls, device: Optional[int] = None) -> "Comm":

@@ -11,6 +11,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "pupperv3-mjx_amd")]
 os.environ.setdefault("PP3_LIB_PATH", os.path.join(ROOT, "pupperv3-mjx_amd", "pupperv3_mjx", "libpupper_hip_prof.so"))
+os.environ.setdefault("PP3_ALLOW_DIAG_BUILD", "1")  # pp3_diag.h: the prof library refuses to run otherwise
 
 import numpy as np  # noqa: E402
 
