@@ -142,24 +142,41 @@ def one_step_err(env, n_sample=256, seed=0, dr_table=None, terrain=None, auto_re
 def contact_cap_stats(env, acts_ptr, steps):
     """Untimed: `steps` env steps with the pipeline record on; counts env steps whose penetrating
     pairs exceed the contact cap (PP3_P_NHIT > the kernel's cap): where the cap binds, the kernel
-    (like the oracle) keeps the deepest and departs from MuJoCo-CPU's keep-all."""
+    (like the oracle) keeps the deepest and departs from MuJoCo-CPU's keep-all.  With
+    obstacle boxes it also counts the sphere-box contacts (box_contacts: env steps whose last
+    substep had one, and their total), i.e. how much of the workload is on the obstacle path."""
     import numpy as np
     from pupperv3_mjx import _abi, _lib
+    m = env.sys_model.struct
+    boxes = np.array([int(m.cgeom_id[g]) for g in range(m.ncgeom)
+                      if m.cgeom_type[g] == _abi.GEOM_BOX and m.cgeom_bodyid[g] == 0])
     cap = env.config_struct.ncon_max or 8
     _lib.check(env._L.pp3_set_pipeline_output(env._h, 1))
     over = 0
     max_hit = 0
     hist = None
+    box_env_steps, box_total = 0, 0
     for i in range(steps):
         env.step_device(acts_ptr + i * env.num_envs * 48)
         p = env._get(_abi.F_PIPELINE)
         nhit = p[:, _abi.P_NHIT].astype(int)
         over += int((nhit > cap).sum())
         max_hit = max(max_hit, int(nhit.max()))
-        hist = np.bincount(p[:, _abi.P_NCON].astype(int), minlength=cap + 1).tolist()
+        ncon = p[:, _abi.P_NCON].astype(int)
+        hist = np.bincount(ncon, minlength=cap + 1).tolist()
+        if boxes.size:
+            g = p[:, _abi.P_CON_GEOM:_abi.P_CON_GEOM + 32].reshape(-1, 16, 2).astype(int)
+            live = np.arange(16)[None, :] < ncon[:, None]
+            nb = (live & (np.isin(g[..., 0], boxes) | np.isin(g[..., 1], boxes))).sum(axis=1)
+            box_env_steps += int((nb > 0).sum())
+            box_total += int(nb.sum())
     _lib.check(env._L.pp3_set_pipeline_output(env._h, 0))
-    return {"cap": int(cap), "env_steps": int(steps * env.num_envs), "overflow_env_steps": over,
-            "max_penetrating_pairs": max_hit, "active_contact_hist_last_step": hist}
+    out = {"cap": int(cap), "env_steps": int(steps * env.num_envs), "overflow_env_steps": over,
+           "max_penetrating_pairs": max_hit, "active_contact_hist_last_step": hist}
+    if boxes.size:
+        out["box_contacts"] = {"env_steps_with_box_contact": box_env_steps, "box_contacts_total": box_total,
+                               "frac_env_steps": round(box_env_steps / (steps * env.num_envs), 4)}
+    return out
 
 
 def cpu_baseline(model, cfg, states, obs, seconds_target=12.0):
@@ -302,6 +319,8 @@ def main():
     ap.add_argument("--obstacles", type=int, default=0, help="obstacles.py boxes (configs[4])")
     ap.add_argument("--terrain", action="store_true",
                     help="per-env terrain (SURVEY 8f rank 3): every env gets its own random boxes in the --obstacles slots")
+    ap.add_argument("--flat-start", action="store_true",
+                    help="with --obstacles: keep the flat start square instead of starting every robot over a box")
     ap.add_argument("--random-commands", action="store_true",
                     help="keep the reset's sampled velocity commands (configs[3]) instead of the fixed (0.5,0,0)")
     ap.add_argument("--gather", action="store_true",
@@ -383,6 +402,17 @@ def main():
     rec = st._record.copy()
     if not args.random_commands:
         rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]
+    if args.obstacles and not args.flat_start:
+        # configs[4]: every robot starts over a box (its own first box with --terrain), so the
+        # workload runs the sphere-box contacts it exists to measure (contact_cap.box_contacts)
+        from pupperv3_mjx import obstacles
+        if terrain is None:
+            specs = obstacles.sample_boxes(args.obstacles, (-5, 5), (-5, 5), 0.02, length=6.0)
+        else:
+            specs = [obstacles.BoxSpec("", float(t[0, 0]), float(t[0, 1]), tuple(float(v) for v in t[0, 3:7]),
+                                       tuple(float(v) for v in t[0, 7:10])) for t in terrain]
+        xy = obstacles.rail_start_xy(specs, E, seed=args.seed * 1000 + rank)
+        rec[:, _abi.S_QPOS:_abi.S_QPOS + 2] = xy
     env._put(_abi.F_STATE, rec)
     init_obs = st.obs.copy()
 
@@ -515,7 +545,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic (actions U(-1,1) pre-generated in HBM; reset keys = jax.random.split(PRNGKey(seed), E))",
             "config": {"workload": ("configs[1]: test_pupper_model.xml, %d envs/GPU, %s, %s, %s"
-                                    % (E, "flat terrain" if not args.obstacles else f"{args.obstacles} obstacle boxes",
+                                    % (E, "flat terrain" if not args.obstacles else
+                                       f"{args.obstacles} obstacle boxes" + ("" if args.flat_start else ", robots started over the boxes"),
                                        "random commands" if args.random_commands else "fixed command (0.5,0,0)",
                                        "domain randomisation" if args.dr else "no DR")),
                        "envs_per_gpu": E, "global_envs": E * world, "obs_history": env._observation_history,

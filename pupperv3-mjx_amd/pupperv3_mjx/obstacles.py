@@ -66,6 +66,26 @@ def add_boxes_to_model(tree: ET.ElementTree, n_boxes: int, x_range: Tuple, y_ran
     return tree
 
 
+def rail_start_xy(specs: Sequence[BoxSpec], num_envs: int, seed: int = 0, offset: float = 0.06,
+                  along: float = 0.8):
+    """Start positions ON the boxes, for workloads that must exercise the sphere-box contacts
+    (BASELINE configs[4]): env i stands over box i % len(specs), at a uniform point of the middle
+    `along` fraction of its long axis (local y, half length half_sizes[1]) and a uniform lateral
+    offset within +-`offset` of its centre line, so its feet land on or beside the rail.  Returns
+    [num_envs, 2] world x, y (numpy Generator seeded with `seed`)."""
+    import numpy as np
+    g = np.random.default_rng(seed)
+    out = np.zeros((num_envs, 2))
+    for i in range(num_envs):
+        b = specs[i % len(specs)]
+        yaw = 2.0 * math.atan2(b.quat[3], b.quat[0])
+        u = g.uniform(-along, along) * b.half_sizes[1]
+        v = g.uniform(-offset, offset)
+        # local y (the rail's length) -> world (-sin, cos); local x (its width) -> (cos, sin)
+        out[i] = [b.x - u * math.sin(yaw) + v * math.cos(yaw), b.y + u * math.cos(yaw) + v * math.sin(yaw)]
+    return out
+
+
 # --------------------------------------------------------------------------- per-env terrain
 # SURVEY 8f rank 3: the reference's boxes are static and shared; here every env may hold its
 # own boxes in the model's box-geom slots (PupperV3Env.set_terrain / pp3_set_terrain).  A row

@@ -32,7 +32,15 @@ def _sample_ids(n, k=64, seed=0):
     return sorted(ids)
 
 
-def _run(require_gpu, n, random_commands, name, model_path=MODEL_XML, dr=False):
+def _box_contacts(st, box_ids):
+    """Per env: number of the last substep's contacts that involve a world box geom."""
+    c = st.pipeline_state.contact
+    live = np.arange(c.geom1.shape[1])[None, :] < c.ncon[:, None]
+    isbox = np.isin(c.geom1, box_ids) | np.isin(c.geom2, box_ids)
+    return (live & isbox).sum(axis=1)
+
+
+def _run(require_gpu, n, random_commands, name, model_path=MODEL_XML, dr=False, start_xy=None, box_ids=None):
     env = PupperV3Env(**bench_kwargs(model_path, random_commands), num_envs=n)
     try:
         table = None
@@ -44,11 +52,18 @@ def _run(require_gpu, n, random_commands, name, model_path=MODEL_XML, dr=False):
         keys = make_keys(7, n)
         st = env.reset(keys)
         if not random_commands:
-            st.info["command"][:] = [0.5, 0.0, 0.0]
+            st.info["command"] = np.tile(np.float32([0.5, 0.0, 0.0]), (n, 1))
+        if start_xy is not None:  # configs[4]: robots stood over the boxes
+            q = st.pipeline_state.q.copy()
+            q[:, 0:2] = start_xy
+            st.pipeline_state.q = q
         rng0 = st.info["rng"].copy()
         rs = np.random.RandomState(1)
+        box_steps = np.zeros(n, dtype=int)  # env steps (of 21) whose last substep touched a box
         for _ in range(20):
             st = env.step(st, rs.uniform(-1, 1, size=(n, 12)).astype(np.float32))
+            if box_ids is not None:
+                box_steps += _box_contacts(st, box_ids) > 0
         # properties over the whole grid
         assert st.obs.shape == (n, 72) and st.reward.shape == (n,) and st.done.shape == (n,)
         for arr in (st.obs, st.reward, st.done, st._record[:, :_abi.S_RNG], st._metrics_raw):
@@ -68,9 +83,21 @@ def _run(require_gpu, n, random_commands, name, model_path=MODEL_XML, dr=False):
         st = env.step(prev, a)
         base = O.OracleEnv(env.sys_model.struct, env.config_struct, precision="f32")
         scales = np.array(env.config_struct.reward_scales[:])
-        fb = G.FlipBudget(max_frac=0.02, name=name)
+        fb = G.FlipBudget(max_frac=0.01, name=name)
         stats = G.TermStats()
-        for i in _sample_ids(n):
+        ids = _sample_ids(n)
+        extra = {}
+        if box_ids is not None:
+            now = _box_contacts(st, box_ids)
+            box_steps += now > 0
+            extra = {"box_contact_envs_any_step": int((box_steps > 0).sum()),
+                     "sampled_envs_with_box_contact": int((box_steps[ids] > 0).sum()),
+                     "sampled_envs_box_contact_compared_step": int((now[ids] > 0).sum()),
+                     "box_contacts_compared_step": int(now[ids].sum())}
+            # the compared envs really are on the obstacle path (verdict r02: a start square
+            # that put robots beside the boxes measured the flat workload)
+            assert extra["sampled_envs_with_box_contact"] >= len(ids) // 4, extra
+        for i in ids:
             oe = base if table is None else O.OracleEnv(env.sys_model.struct, env.config_struct, dr=table[i],
                                                          precision="f32")
             o = oe.step(dict(state=G.record_to_oracle_state(prev._record[i]), obs=prev.obs[i].astype(np.float64)),
@@ -89,7 +116,7 @@ def _run(require_gpu, n, random_commands, name, model_path=MODEL_XML, dr=False):
                 stats.add(errs)
             flip = o["boundary"] > 0 or G.foot_threshold_flip(o["pipe"], env.config_struct.foot_radius)
             fb.check(not bad, dict(o, boundary=int(flip)), f"env {i}: {bad}")
-        G.report(name, {"envs": n, "worst": {k: float(f"{v:.3g}") for k, v in stats.worst.items()}})
+        G.report(name, {"envs": n, **extra, "worst": {k: float(f"{v:.3g}") for k, v in stats.worst.items()}})
         fb.finish()
     finally:
         env.close()
@@ -108,14 +135,28 @@ def test_configs2_4096_envs_domain_randomised(require_gpu):
 
 
 def test_configs4_4096_envs_obstacle_boxes(require_gpu, tmp_path):
-    """configs[4] per GPU: the 10 obstacles.py boxes of the golden layout (seed 0) in the model."""
+    """configs[4] per GPU: the 10 obstacles.py boxes of the golden layout (seed 0,
+    test_environment.py:18-43: x, y in (-5, 5), length 6) in the model, every robot started over a
+    box (obstacles.rail_start_xy) so the sphere-box lanes, variable contact counts and the solver
+    work they bring are what the 64 compared envs exercise; the sphere-box contacts are counted
+    from the pipeline record and at least a quarter of the compared envs must have had one."""
     import xml.etree.ElementTree as ET
     from pupperv3_mjx import obstacles
     tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
-    obstacles.add_boxes_to_model(tree, n_boxes=10, x_range=(-5, 5), y_range=(-5, 5), height=0.02, length=6.0)
+    kw = dict(n_boxes=10, x_range=(-5, 5), y_range=(-5, 5), height=0.02, length=6.0)
+    obstacles.add_boxes_to_model(tree, **kw)
     path = str(tmp_path / "pupper_obstacles.xml")
     tree.write(path, encoding="unicode")
-    _run(require_gpu, 4096, False, "headline_4096_obstacles", model_path=path)
+    specs = obstacles.sample_boxes(kw["n_boxes"], kw["x_range"], kw["y_range"], kw["height"], length=kw["length"])
+    n = 4096
+    _run(require_gpu, n, False, "headline_4096_obstacles", model_path=path,
+         start_xy=obstacles.rail_start_xy(specs, n, seed=3), box_ids=_world_box_geoms(path))
+
+
+def _world_box_geoms(path):
+    env_model = common.env_model_and_config(path)[0]
+    return np.array([int(env_model.cgeom_id[g]) for g in range(env_model.ncgeom)
+                     if env_model.cgeom_type[g] == _abi.GEOM_BOX and env_model.cgeom_bodyid[g] == 0])
 
 
 def test_odd_batch_4097_envs(require_gpu):

@@ -125,3 +125,20 @@ def test_terrain_from_specs_equals_model_boxes(tmp_path):
         a = O.mj_step(m, qpos[i], qvel[i], qws[i], ctrl[i], nsteps=2)
         b = O.mj_step(mt, qpos[i], qvel[i], qws[i], ctrl[i], nsteps=2)
         np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-6)
+
+
+def test_rail_start_xy_on_the_boxes():
+    """configs[4] starts (bench.py --obstacles, test_gpu_headline): each position lies over its box,
+    within the lateral offset of the centre line and the middle `along` fraction of its length."""
+    import math
+    import numpy as np
+    specs = obstacles.sample_boxes(10, (-5, 5), (-5, 5), 0.02, length=6.0)
+    xy = obstacles.rail_start_xy(specs, 500, seed=1, offset=0.06, along=0.8)
+    for i, (x, y) in enumerate(xy):
+        b = specs[i % 10]
+        yaw = 2.0 * math.atan2(b.quat[3], b.quat[0])
+        dx, dy = x - b.x, y - b.y
+        lx = dx * math.cos(yaw) + dy * math.sin(yaw)   # across the rail
+        ly = -dx * math.sin(yaw) + dy * math.cos(yaw)  # along the rail
+        assert abs(lx) <= 0.06 + 1e-12 and abs(ly) <= 0.8 * 3.0 + 1e-12
+    assert np.ptp(xy[:, 0]) > 1.0  # spread over the field, not one spot
