@@ -179,6 +179,36 @@ def contact_cap_stats(env, acts_ptr, steps):
     return out
 
 
+def host_api_rates(model_path, E, device, keys, steps=30, warmup=3):
+    """Untimed extra (verdict r02 item 5): the drop-in host surface -- `env.step(state, action)` and
+    `wrappers.wrap(env).step` with numpy actions and the State returned to the host every step
+    (obs / reward / done copied at once, the rest lazily; an unedited state is not re-uploaded) --
+    at the bench's env count, with the constructor's default pipeline record and without it."""
+    import numpy as np
+    from pupperv3_mjx import wrappers
+    from pupperv3_mjx.environment import PupperV3Env
+    acts = np.random.RandomState(3).uniform(-1, 1, size=(warmup + steps, E, 12)).astype(np.float32)
+    out = {}
+    for pipe in (True, False):
+        for wrapped in (False, True):
+            env = PupperV3Env(**bench_kwargs(model_path), num_envs=E, device=device, pipeline_output=pipe)
+            api = wrappers.wrap(env, episode_length=1000) if wrapped else env
+            st = api.reset(keys)
+            for i in range(warmup):
+                st = api.step(st, acts[i])
+            t = time.perf_counter()
+            for i in range(steps):
+                st = api.step(st, acts[warmup + i])
+            dt = time.perf_counter() - t
+            out[("wrap(env).step" if wrapped else "env.step") + ("" if pipe else " [pipeline_output=False]")] = round(
+                E * steps / dt, 1)
+            env.close()
+    out["per_step_pcie_bytes"] = {"h2d_actions": E * 12 * 4, "d2h_obs_reward_done": E * (72 + 2) * 4}
+    out["note"] = ("env-steps/s through the host API (numpy in, numpy out, one host sync per step); the device "
+                   "path is `value`")
+    return out
+
+
 def cpu_baseline(model, cfg, states, obs, seconds_target=12.0):
     """Time the oracle (C fp64 restatement of the same step, OpenMP over envs) on host cores."""
     import numpy as np
@@ -602,6 +632,8 @@ def main():
                                           "ratio": round(launch_s / half_s, 4),
                                           "note": "launch time at E / at E/2 envs (one wave per SIMD)"}
         if world == 1 and not args.no_extras:
+            if not (args.dr or args.obstacles or args.auto_reset or args.policy or args.gather):
+                out["host_api"] = host_api_rates(model_path, E, device, keys)
             out["contact_cap"] = contact_cap_stats(env, acts.ptr.value, min(K, 50))
             out["one_step_err"] = one_step_err(env, dr_table=dr_table, terrain=terrain, auto_reset=args.auto_reset > 0)
             out["qpos_rel_err"] = {"value": qpos_drift(env, dr_row=None if dr_table is None else dr_table[0],

@@ -7,10 +7,13 @@ numbers), all forced by the device-resident design:
 
 * the env is batched: ``PupperV3Env(..., num_envs=N)``; ``reset(rng)`` takes N keys [N, 2]
   (or one key [2] when N == 1) and ``step(state, action)`` takes actions [N, 12];
-* ``State`` fields are numpy host copies (``obs`` [N, 36H], ``reward`` [N], ``done`` [N],
-  ``metrics``/``info`` dicts of [N, ...] arrays); ``step`` packs ``state.info`` / qpos / qvel
-  back into the device record first, so editing ``state.info["command"]`` works as in
-  test_environment.py:291;
+* ``State`` fields are numpy host arrays (``obs`` [N, 36H], ``reward`` [N], ``done`` [N],
+  ``metrics``/``info`` dicts of [N, ...] arrays), read-only like the reference's immutable JAX
+  arrays: a state is edited by assigning new arrays (``state.info["command"] = ...``, as
+  test_environment.py:147,186 do), and ``step`` packs an edited state back into the device record;
+* reset/step return a ``DeviceState``: obs / reward / done are copied to the host at once, the
+  rest (info, metrics, pipeline_state) on first access; a state passed back to ``step`` unedited
+  (the usual rollout loop) is not re-uploaded -- the device already holds it;
 * the zero-copy path for training loops is ``step_device`` / ``device_fields`` (no host
   round trip); ``State.pipeline_state`` exposes q, qd, x, xd, site_xpos, qfrc_actuator and
   contacts of the last substep (brax State semantics, environment.py:367).
@@ -19,6 +22,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import weakref
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -78,6 +82,69 @@ class State:
     done: np.ndarray
     metrics: Dict[str, np.ndarray] = field(default_factory=dict)
     info: Dict[str, Any] = field(default_factory=dict)
+
+
+_LAZY = ("pipeline_state", "metrics", "info", "_record", "_metrics_raw")
+
+
+def _ro(a):
+    """Read-only view of a host array handed out in a State (JAX arrays are immutable)."""
+    a = np.asarray(a)
+    a.flags.writeable = False
+    return a
+
+
+class DeviceState(State):
+    """A State returned by PupperV3Env.reset / step (the host surface of the
+    device-resident env).  obs / reward / done are host arrays from the start; pipeline_state,
+    metrics, info (and the raw record) are downloaded on first access -- from the env's live
+    buffers while the env has not launched since, else from a device snapshot the env took just
+    before its next launch (PupperV3Env._before_launch), so an old state always reads its own data.
+    Every array is read-only; ``unedited()`` tells the env whether the device still holds exactly
+    this state (then step() skips the upload)."""
+
+    def __init__(self, env: "PupperV3Env", gen: int, single: bool, obs, reward, done):
+        self.__dict__.update(obs=obs, reward=reward, done=done, _env=env, _gen=gen, _single=single, _snap=None,
+                             _ids=None, _out=(obs, reward, done))
+
+    def __getattr__(self, name):
+        if name in _LAZY and "_env" in self.__dict__:
+            self._materialize()
+            return self.__dict__[name]
+        raise AttributeError(name)
+
+    @property
+    def materialized(self) -> bool:
+        return "info" in self.__dict__
+
+    def _materialize(self) -> None:
+        if self.materialized:
+            return
+        env = self._env
+        src = self._snap
+        if src is None and env._gen != self._gen:
+            raise RuntimeError("DeviceState: the env launched again without preserving this state (internal error)")
+        fields = env._lazy_fields()
+        got = {}
+        for f in fields:
+            got[f] = env._download(f, src.ptr.value + env._snap_offsets[f] if src is not None else None)
+        self.__dict__.update(env._unpack_lazy(self, got, self._single))
+        self.__dict__["_ids"] = _identity(self)
+        if src is not None:
+            env._snap_pool.append(src)
+            self.__dict__["_snap"] = None
+
+    def unedited(self) -> bool:
+        """True when every array step() would upload is the very object this state was issued with."""
+        if tuple(self.__dict__.get(k) for k in ("obs", "reward", "done")) != self._out:
+            return False
+        return not self.materialized or _identity(self) == self._ids
+
+
+def _identity(st) -> tuple:
+    ps, info = st.__dict__["pipeline_state"], st.__dict__["info"]
+    return (id(ps), id(ps.q), id(ps.qd), id(ps.qacc_warmstart), id(info),
+            tuple((k, id(v)) for k, v in info.items()), id(st.__dict__["obs"]))
 
 
 _DEFAULT_LOWER = [-1.220, -0.420, -2.790, -2.510, -3.140, -0.710, -1.220, -0.420, -2.790, -2.510, -3.140, -0.710]
@@ -255,6 +322,22 @@ class PupperV3Env:
         self._keys_buf = _lib.DeviceBuffer(self.num_envs * 8, self.device)
         self._act_buf = _lib.DeviceBuffer(self.num_envs * _abi.NU * 4, self.device)
         self._dr_buf = None
+        self._init_host_state()
+
+    def _init_host_state(self) -> None:
+        """Bookkeeping of the lazy host surface (DeviceState): generation counter of the device
+        buffers, the last issued state, and a pool of device snapshots of its lazy fields."""
+        self._gen = 0
+        self._issued = None
+        self._snap_pool = []
+        self._lazy_extra = {}  # field id -> info hook (wrappers.AutoResetEpisodeEnv: the episode record)
+        self._field_elems = {f: self.device_field(f)[1] for f in (_abi.F_STATE, _abi.F_METRICS, _abi.F_PIPELINE)}
+        self._field_elems[_abi.F_EPISODE] = _abi.EP_STRIDE
+        off, self._snap_offsets = 0, {}
+        for f in (_abi.F_STATE, _abi.F_METRICS, _abi.F_PIPELINE, _abi.F_EPISODE):
+            self._snap_offsets[f] = off
+            off += (self.num_envs * self._field_elems[f] * 4 + 255) // 256 * 256
+        self._snap_bytes = off
 
     # ------------------------------------------------------------------ reference helpers
     def sample_command(self, rng) -> np.ndarray:
@@ -387,10 +470,12 @@ class PupperV3Env:
         return p.value, n.value
 
     def reset_device(self, keys_dev: int, mask_dev: Optional[int] = None, stream: Optional[int] = None) -> None:
+        self._before_launch()
         _lib.check(self._L.pp3_reset(self._h, C.c_void_p(keys_dev), C.c_void_p(mask_dev) if mask_dev else None,
                                      C.c_void_p(stream) if stream else None))
 
     def step_device(self, actions_dev: int, stream: Optional[int] = None) -> None:
+        self._before_launch()
         _lib.check(self._L.pp3_step(self._h, C.c_void_p(actions_dev), C.c_void_p(stream) if stream else None))
 
     def synchronize(self) -> None:
@@ -403,6 +488,7 @@ class PupperV3Env:
         return out
 
     def _put(self, field_id: int, arr: np.ndarray) -> None:
+        self._before_launch()
         a = np.ascontiguousarray(arr, dtype=np.float32)
         _lib.check(self._L.pp3_copy_field_from_host(self._h, field_id, a.ctypes.data_as(C.c_void_p), a.nbytes))
 
@@ -419,17 +505,62 @@ class PupperV3Env:
         keys, single = self._batch_keys(rng)
         self._keys_buf.upload(keys)
         self.reset_device(self._keys_buf.ptr.value)
-        self.synchronize()
-        return self._read_state(single)
+        return self._issue(single)
 
     def step(self, state: State, action) -> State:
         single = np.ndim(state.reward) == 0
         act = np.ascontiguousarray(np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU))
-        self._write_state(state)
+        if not self.holds(state):
+            self._write_state(state)
         self._act_buf.upload(act)
         self.step_device(self._act_buf.ptr.value)
+        return self._issue(single)
+
+    def holds(self, state: State) -> bool:
+        """The device buffers hold exactly `state`: the last state this env issued, unedited, and
+        no launch or upload since."""
+        return (isinstance(state, DeviceState) and state.__dict__.get("_env") is self and state._gen == self._gen
+                and state.unedited())
+
+    # lazy host state: obs / reward / done now, the rest on first access (DeviceState)
+    def _lazy_fields(self) -> Tuple[int, ...]:
+        return ((_abi.F_STATE, _abi.F_METRICS) + ((_abi.F_PIPELINE,) if self._pipeline_output else ())
+                + tuple(self._lazy_extra))
+
+    def _download(self, field_id: int, src_dev: Optional[int] = None) -> np.ndarray:
+        if src_dev is None:
+            return self._get(field_id)
+        n = self._field_elems[field_id]
+        out = np.empty((self.num_envs, n), dtype=np.float32)
+        _lib.check(self._L.pp3_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(src_dev), out.nbytes))
+        return out
+
+    def _issue(self, single: bool) -> DeviceState:
         self.synchronize()
-        return self._read_state(single)
+        obs = _ro(self._get(_abi.F_OBS))
+        rew = _ro(self._get(_abi.F_REWARD)[:, 0])
+        done = _ro(self._get(_abi.F_DONE)[:, 0])
+        if single:
+            obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
+        st = DeviceState(self, self._gen, single, obs, rew, done)
+        self._issued = weakref.ref(st)
+        return st
+
+    def _before_launch(self) -> None:
+        """Called before anything changes the device buffers: the last issued state, if still alive
+        and not yet downloaded, gets a device-side snapshot of its lazy fields (d2d copies on the
+        env's stream, ordered before the launch), then the buffers' generation advances."""
+        st = self._issued() if self._issued is not None else None
+        if st is not None and not st.materialized and st._snap is None and st._gen == self._gen:
+            buf = self._snap_pool.pop() if self._snap_pool else _lib.DeviceBuffer(self._snap_bytes, self.device)
+            stream = self._L.pp3_stream(self._h)
+            for f in self._lazy_fields():
+                ptr, n = self.device_field(f)
+                _lib.check(self._L.pp3_memcpy_d2d(C.c_void_p(buf.ptr.value + self._snap_offsets[f]), C.c_void_p(ptr),
+                                                  self.num_envs * n * 4, C.c_void_p(stream)))
+            st.__dict__["_snap"] = buf
+            weakref.finalize(st, _return_snapshot, self._snap_pool, st.__dict__)
+        self._gen += 1
 
     # ------------------------------------------------------------------ packing
     def _unpack_info(self, rec: np.ndarray) -> Dict[str, Any]:
@@ -451,12 +582,10 @@ class PupperV3Env:
         }
         return info
 
-    def _read_state(self, single: bool) -> State:
-        rec = self._get(_abi.F_STATE)
-        obs = self._get(_abi.F_OBS)
-        rew = self._get(_abi.F_REWARD)[:, 0]
-        done = self._get(_abi.F_DONE)[:, 0]
-        met = self._get(_abi.F_METRICS)
+    def _unpack_lazy(self, st: "DeviceState", got: Dict[int, np.ndarray], single: bool) -> Dict[str, Any]:
+        """The lazy part of a DeviceState from its downloaded record / metrics / pipeline rows."""
+        rec = got[_abi.F_STATE]
+        met = got[_abi.F_METRICS]
         info = self._unpack_info(rec)
         info["rewards"] = {k: met[:, 1 + i] for i, k in enumerate(_abi.REWARD_NAMES)}
         metrics = {"total_dist": met[:, 0]}
@@ -464,7 +593,7 @@ class PupperV3Env:
         ps = PipelineState(q=rec[:, _abi.S_QPOS:_abi.S_QPOS + 19].copy(), qd=rec[:, _abi.S_QVEL:_abi.S_QVEL + 18].copy(),
                            qacc_warmstart=rec[:, _abi.S_QACC_WS:_abi.S_QACC_WS + 18].copy())
         if self._pipeline_output:
-            p = self._get(_abi.F_PIPELINE)
+            p = got[_abi.F_PIPELINE]
             nb = _abi.NBODY - 1
             ps.x = Transform(pos=p[:, _abi.P_XPOS:_abi.P_XPOS + 3 * nb].reshape(-1, nb, 3),
                              rot=p[:, _abi.P_XQUAT:_abi.P_XQUAT + 4 * nb].reshape(-1, nb, 4))
@@ -479,12 +608,15 @@ class PupperV3Env:
             ps.contact.ncon = ncon
             ps.subtree_com = p[:, _abi.P_SUBTREE_COM:_abi.P_SUBTREE_COM + 3]
             ps.sensordata = p[:, _abi.P_SENSOR:_abi.P_SENSOR + self.sys_model.struct.nsensordata]
-        st = State(pipeline_state=ps, obs=obs, reward=rew, done=done, metrics=metrics, info=info)
-        st._record = rec
-        st._metrics_raw = met  # [N][19]: total_dist, then the scaled terms in _abi.REWARD_NAMES order
         if single:
-            st = _squeeze(st)
-        return st
+            sq = _squeeze_tree
+            ps, metrics, info = sq(ps), sq(metrics), sq(info)
+        for fid, hook in self._lazy_extra.items():  # wrappers' info entries (wrappers.py)
+            info.update(hook(st, got, single))
+        _freeze(ps)
+        _freeze(metrics)
+        _freeze(info)
+        return dict(pipeline_state=ps, metrics=metrics, info=info, _record=_ro(rec), _metrics_raw=_ro(met))
 
     def _write_state(self, state: State) -> None:
         rec = getattr(state, "_record", None)
@@ -519,32 +651,36 @@ class PupperV3Env:
         self._put(_abi.F_OBS, np.asarray(state.obs, dtype=np.float32).reshape(n, -1))
 
 
-def _squeeze(st: State) -> State:
-    """Drop the leading batch axis of a 1-env State (single-key reset API)."""
-
-    def sq(v):
-        if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == 1:
-            return v[0]
-        if isinstance(v, dict):
-            return {k: sq(x) for k, x in v.items()}
+def _squeeze_tree(v):
+    """Drop the leading batch axis of a 1-env result (single-key reset API)."""
+    if isinstance(v, np.ndarray):
+        return v[0] if v.ndim >= 1 and v.shape[0] == 1 else v
+    if isinstance(v, dict):
+        return {k: _squeeze_tree(x) for k, x in v.items()}
+    if isinstance(v, (PipelineState, Transform, Motion, Contact)):
+        for k, x in list(vars(v).items()):
+            setattr(v, k, _squeeze_tree(x))
         return v
+    return v
 
-    ps = st.pipeline_state
-    ps2 = PipelineState(q=sq(ps.q), qd=sq(ps.qd), qacc_warmstart=sq(ps.qacc_warmstart))
-    if ps.x is not None:
-        ps2.x = Transform(sq(ps.x.pos), sq(ps.x.rot))
-        ps2.xd = Motion(sq(ps.xd.vel), sq(ps.xd.ang))
-        ps2.site_xpos = sq(ps.site_xpos)
-        ps2.qfrc_actuator = sq(ps.qfrc_actuator)
-        ps2.qacc = sq(ps.qacc)
-        ps2.contact = Contact(sq(ps.contact.dist), sq(ps.contact.geom1), sq(ps.contact.geom2))
-        ps2.subtree_com = sq(ps.subtree_com)
-        ps2.sensordata = sq(ps.sensordata)
-    out = State(pipeline_state=ps2, obs=sq(st.obs), reward=sq(st.reward), done=sq(st.done),
-                metrics=sq(st.metrics), info=sq(st.info))
-    out._record = st._record
-    out._metrics_raw = st._metrics_raw
-    return out
+
+def _freeze(v):
+    """Every array of a State tree read-only (in place)."""
+    if isinstance(v, np.ndarray):
+        v.flags.writeable = False
+    elif isinstance(v, dict):
+        for x in v.values():
+            _freeze(x)
+    elif isinstance(v, (PipelineState, Transform, Motion, Contact)):
+        for x in vars(v).values():
+            _freeze(x)
+
+
+def _return_snapshot(pool, d) -> None:
+    """weakref finalizer of a DeviceState: its device snapshot (if any) goes back to the env's pool."""
+    buf = d.get("_snap")
+    if buf is not None:
+        pool.append(buf)
 
 
 def make_keys(seed: int, n: int, partitionable: bool = True) -> np.ndarray:

@@ -44,6 +44,8 @@ class AutoResetEpisodeEnv:
         self.action_repeat = int(action_repeat)
         _lib.check(env._L.pp3_set_auto_reset(env._h, self.episode_length))
         _lib.check(env._L.pp3_set_action_repeat(env._h, self.action_repeat))
+        env._lazy_extra = {_abi.F_EPISODE: self._extra_info}  # info entries of the env's DeviceStates
+        self._first_ps, self._first_obs = None, None
 
     # brax Env surface
     @property
@@ -62,37 +64,45 @@ class AutoResetEpisodeEnv:
     def unwrapped(self) -> PupperV3Env:
         return self.env
 
-    def _decorate(self, st: State) -> State:
-        ep = self.env._get(_abi.F_EPISODE)
-        first = self.env._get(_abi.F_FIRST_STATE)
-        fobs = self.env._get(_abi.F_FIRST_OBS)
-        single = np.ndim(st.reward) == 0
+    def _extra_info(self, st, got, single: bool) -> dict:
+        """The wrapper's info entries of a DeviceState, built when its lazy part is downloaded: the
+        episode record rides along as one more lazy field (snapshotted with the rest); the first
+        state / obs change only at reset and are cached on the host then."""
+        ep = got[_abi.F_EPISODE]
         sq = (lambda v: v[0]) if single else (lambda v: v)
-        st.info["steps"] = sq(ep[:, _abi.EP_STEPS].copy())
-        st.info["truncation"] = sq(ep[:, _abi.EP_TRUNCATION].copy())
-        st.info["episode_metrics"] = {"sum_reward": sq(ep[:, _abi.EP_SUM_REWARD].copy()),
-                                      "length": sq(ep[:, _abi.EP_LENGTH].copy())}
-        st.info["episode_done"] = sq(np.asarray(st.reward) * 0 + np.asarray(st.done))
-        st.info["first_pipeline_state"] = {"q": sq(first[:, 0:19].copy()), "qd": sq(first[:, 19:37].copy()),
-                                           "qacc_warmstart": sq(first[:, 37:55].copy())}
-        st.info["first_obs"] = sq(fobs.copy())
-        return st
+        return {"steps": sq(ep[:, _abi.EP_STEPS].copy()),
+                "truncation": sq(ep[:, _abi.EP_TRUNCATION].copy()),
+                "episode_metrics": {"sum_reward": sq(ep[:, _abi.EP_SUM_REWARD].copy()),
+                                    "length": sq(ep[:, _abi.EP_LENGTH].copy())},
+                "episode_done": np.array(st.done, dtype=np.float32),
+                "first_pipeline_state": self._first_ps,
+                "first_obs": self._first_obs}
 
     def reset(self, rng) -> State:
-        return self._decorate(self.env.reset(rng))
+        st = self.env.reset(rng)
+        sq = (lambda v: v[0]) if np.ndim(st.reward) == 0 else (lambda v: v)
+        first = self.env._get(_abi.F_FIRST_STATE)
+        fobs = self.env._get(_abi.F_FIRST_OBS)
+        self._first_ps = {"q": sq(first[:, 0:19].copy()), "qd": sq(first[:, 19:37].copy()),
+                          "qacc_warmstart": sq(first[:, 37:55].copy())}
+        self._first_obs = sq(fobs.copy())
+        return st
 
     def step(self, state: State, action) -> State:
         n = self.env.num_envs
-        info = state.info
-        if "steps" in info:  # host-side edits of the episode record are honoured
-            ep = np.zeros((n, _abi.EP_STRIDE), dtype=np.float32)
-            ep[:, _abi.EP_STEPS] = np.asarray(info["steps"], dtype=np.float32).reshape(n)
-            ep[:, _abi.EP_TRUNCATION] = np.asarray(info["truncation"], dtype=np.float32).reshape(n)
-            ep[:, _abi.EP_SUM_REWARD] = np.asarray(info["episode_metrics"]["sum_reward"], dtype=np.float32).reshape(n)
-            ep[:, _abi.EP_LENGTH] = np.asarray(info["episode_metrics"]["length"], dtype=np.float32).reshape(n)
-            self.env._put(_abi.F_EPISODE, ep)
-        self.env._put(_abi.F_DONE, np.asarray(state.done, dtype=np.float32).reshape(n, 1))
-        return self._decorate(self.env.step(state, action))
+        if not self.env.holds(state):
+            # an edited (or foreign) state: its episode record and done go back with it (env.step
+            # then uploads the rest); the rollout loop's unedited states skip all of this
+            info = state.info
+            if "steps" in info:
+                ep = np.zeros((n, _abi.EP_STRIDE), dtype=np.float32)
+                ep[:, _abi.EP_STEPS] = np.asarray(info["steps"], dtype=np.float32).reshape(n)
+                ep[:, _abi.EP_TRUNCATION] = np.asarray(info["truncation"], dtype=np.float32).reshape(n)
+                ep[:, _abi.EP_SUM_REWARD] = np.asarray(info["episode_metrics"]["sum_reward"], dtype=np.float32).reshape(n)
+                ep[:, _abi.EP_LENGTH] = np.asarray(info["episode_metrics"]["length"], dtype=np.float32).reshape(n)
+                self.env._put(_abi.F_EPISODE, ep)
+            self.env._put(_abi.F_DONE, np.asarray(state.done, dtype=np.float32).reshape(n, 1))
+        return self.env.step(state, action)
 
 
 def wrap(env: PupperV3Env, episode_length: int = 1000, action_repeat: int = 1,

@@ -191,4 +191,5 @@ def env_with_model(path, model_struct, n, **kw):
     e._keys_buf = _lib.DeviceBuffer(n * 8, 0)
     e._act_buf = _lib.DeviceBuffer(n * _abi.NU * 4, 0)
     e._dr_buf = None
+    e._init_host_state()
     return e

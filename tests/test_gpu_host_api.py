@@ -1,0 +1,127 @@
+"""The drop-in host surface (environment.py:314,348 reset/step returning a State) over
+the device-resident env: DeviceState semantics.
+
+* an unedited state passed back to step() is not re-uploaded, and the rollout equals one in which
+  every state is re-uploaded from the host, bit for bit;
+* old states keep their own data after the env has stepped on (device snapshots of the lazy part);
+* an edited state (a new array assigned, as test_environment.py:147,186 do) is uploaded and
+  honoured; in-place edits are refused (read-only arrays, as JAX arrays are immutable);
+* the same through wrappers.wrap (EpisodeWrapper + AutoResetWrapper on device).
+"""
+import numpy as np
+import pytest
+
+import common
+from pupperv3_mjx import MODEL_XML, _abi, wrappers
+from pupperv3_mjx.environment import PupperV3Env, make_keys
+
+pytestmark = pytest.mark.gpu
+N = 64
+
+
+def _env(**kw):
+    return PupperV3Env(**common.fixture_kwargs(MODEL_XML, **kw), num_envs=N)
+
+
+def _count_uploads(env):
+    calls = []
+    orig = env._write_state
+
+    def spy(st):
+        calls.append(1)
+        return orig(st)
+    env._write_state = spy
+    return calls
+
+
+def test_unedited_states_are_not_reuploaded_and_match_forced_uploads(require_gpu):
+    acts = np.random.RandomState(0).uniform(-1, 1, size=(12, N, 12)).astype(np.float32)
+    e1, e2 = _env(), _env()
+    try:
+        uploads = _count_uploads(e1)
+        s1, s2 = e1.reset(make_keys(4, N)), e2.reset(make_keys(4, N))
+        for t in range(12):
+            s1 = e1.step(s1, acts[t])
+            if t % 3 == 0:
+                _ = s1.info["rng"]  # materialised states stay "held" while unedited
+            e2._write_state(s2)  # forced host round trip of every state
+            s2 = e2.step(e2._issue(False), acts[t])
+        assert not uploads
+        np.testing.assert_array_equal(s1.obs, s2.obs)
+        np.testing.assert_array_equal(s1.reward, s2.reward)
+        np.testing.assert_array_equal(s1._record, s2._record)
+    finally:
+        e1.close()
+        e2.close()
+
+
+def test_old_states_keep_their_data(require_gpu):
+    e = _env()
+    try:
+        st = e.reset(make_keys(5, N))
+        rs = np.random.RandomState(1)
+        kept, eager = [], []
+        for t in range(6):
+            st = e.step(st, rs.uniform(-1, 1, size=(N, 12)).astype(np.float32))
+            kept.append(st)
+            eager.append((e._get(_abi.F_STATE).copy(), e._get(_abi.F_METRICS).copy(), e._get(_abi.F_PIPELINE).copy()))
+        for st, (rec, met, pipe) in zip(kept, eager):  # read only now, after the env moved on
+            np.testing.assert_array_equal(st._record, rec)
+            np.testing.assert_array_equal(st._metrics_raw, met)
+            np.testing.assert_array_equal(st.pipeline_state.q, rec[:, :19])
+            np.testing.assert_array_equal(st.pipeline_state.qacc, pipe[:, _abi.P_QACC:_abi.P_QACC + 18])
+            assert np.all(st.info["step"] == rec[:, _abi.S_STEP].astype(np.int32))
+        # stepping an OLD state rewinds the env to it (it is uploaded from its snapshot)
+        a = np.zeros((N, 12), dtype=np.float32)
+        r1 = e.step(kept[2], a)
+        r2 = e.step(kept[2], a)
+        np.testing.assert_array_equal(r1._record, r2._record)
+    finally:
+        e.close()
+
+
+def test_edited_state_is_uploaded_and_inplace_edits_refused(require_gpu):
+    e = _env(resample_velocity_step=10 ** 9)
+    try:
+        st = e.reset(make_keys(6, N))
+        with pytest.raises(ValueError):
+            st.info["command"][0, 0] = 9.0  # read-only, as the reference's jax arrays
+        with pytest.raises(ValueError):
+            st.obs[0, 0] = 1.0
+        st.info["command"] = np.tile(np.float32([0.3, -0.2, 0.1]), (N, 1))
+        assert not e.holds(st)
+        out = e.step(st, np.zeros((N, 12), dtype=np.float32))
+        np.testing.assert_array_equal(out.info["command"], np.tile(np.float32([0.3, -0.2, 0.1]), (N, 1)))
+        assert e.holds(out)
+    finally:
+        e.close()
+
+
+def test_wrapper_rollout_without_uploads_matches_forced(require_gpu):
+    acts = np.random.RandomState(2).uniform(-1, 1, size=(20, N, 12)).astype(np.float32)
+    e1, e2 = _env(terminal_body_z=0.3), _env(terminal_body_z=0.3)
+    try:
+        w1, w2 = wrappers.wrap(e1, episode_length=7), wrappers.wrap(e2, episode_length=7)
+        uploads = _count_uploads(e1)
+        s1, s2 = w1.reset(make_keys(8, N)), w2.reset(make_keys(8, N))
+        for t in range(20):
+            s1 = w1.step(s1, acts[t])
+            s2 = dict_roundtrip(w2, s2)
+            s2 = w2.step(s2, acts[t])
+            np.testing.assert_array_equal(s1.done, s2.done)
+        assert not uploads
+        np.testing.assert_array_equal(s1.obs, s2.obs)
+        for k in ("steps", "truncation"):
+            np.testing.assert_array_equal(s1.info[k], s2.info[k])
+        np.testing.assert_array_equal(s1.info["episode_metrics"]["sum_reward"], s2.info["episode_metrics"]["sum_reward"])
+    finally:
+        e1.close()
+        e2.close()
+
+
+def dict_roundtrip(w, st):
+    """A state rebuilt on the host (every array a fresh copy): the wrapper must upload it."""
+    info = {k: (dict(v) if isinstance(v, dict) else np.array(v)) for k, v in st.info.items()}
+    st.info = info
+    assert not w.env.holds(st)
+    return st

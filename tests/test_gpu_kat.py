@@ -59,3 +59,73 @@ def test_kernel_frictionloss_slip(require_gpu):
     expect = (tau - np.sign(tau) * m.dof_frictionloss[KNEE] - m.dof_damping[KNEE] * vm) / Mkk
     np.testing.assert_allclose(acc, expect, rtol=1.5e-2)
     assert np.all(np.abs(out[1][1][:, 6:8]).max(axis=1) < 1e-2 * np.abs(v2))  # parents held
+
+
+# ------------------------------------------------------------------ pyramidal friction (ball)
+import test_friction_kat as F  # noqa: E402
+
+
+def _ball_gpu(m, nsteps, n=2):
+    """The ball model (test_friction_kat.ball_model) on the kernel: n identical envs from rest."""
+    e = G.env_with_model(common.MODEL_XML, m, n)
+    try:
+        q, v, w = F._rest_state()
+        tile = lambda x: np.tile(x, (n, 1))  # noqa: E731
+        out = [G.gpu_physics(e, tile(q), tile(v), tile(w), tile(F.DP), k) for k in nsteps]
+        return [(o[0][0], o[1][0], o[2][0]) for o in out]
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("case", sorted(F.CASES))
+def test_kernel_converged_qacc_equals_documented_soft_pyramid(require_gpu, case):
+    """The kernel's pyramid edge rows, impratio regulariser and aref: with Newton run to convergence
+    its qacc at a rolling / sliding state equals the exact minimiser of the documented problem
+    (fp32: 2e-3 relative to g)."""
+    theta, mu = F.CASES[case]
+    m = F.ball_model(theta, mu, iterations=50)
+    (q, v, w), = _ball_gpu(m, [150])
+    e = G.env_with_model(common.MODEL_XML, m, 2)
+    try:
+        _, _, w2, _ = G.gpu_physics(e, np.tile(q, (2, 1)), np.tile(v, (2, 1)), np.tile(w, (2, 1)),
+                                    np.tile(F.DP, (2, 1)), 1)
+    finally:
+        e.close()
+    a, info = F.ball_qacc(m, q, v)
+    assert info["dist"] < 0 and sum(info["active"]) >= 1
+    np.testing.assert_allclose(w2[0, 0:6], a, atol=2e-3 * F.G + 2e-3 * np.abs(a))
+
+
+def test_kernel_ball_rolls_at_five_sevenths_g_sin(require_gpu):
+    """The reference's solver (iterations = 1) on the kernel: rolling at (5/7) g sin th, contact
+    point creeping at < 0.1 % of the speed."""
+    theta, mu = F.CASES["roll"]
+    m = F.ball_model(theta, mu)
+    (q1, v1, _), (q2, v2, _) = _ball_gpu(m, [100, 150])
+    acc = (v2[0] - v1[0]) / (50 * m.timestep)
+    np.testing.assert_allclose(acc, 5.0 / 7.0 * F.G * np.sin(np.radians(theta)), rtol=5e-3)
+    assert abs(F._slip(q2, v2)[0]) < 1e-3 * v2[0]
+
+
+def test_kernel_ball_slides_at_the_coulomb_bound(require_gpu):
+    """mu below the stick threshold (converged Newton): the kernel's ball accelerates at
+    g (sin th - mu cos th) over a long slide, spinning up from the friction torque."""
+    theta, mu = F.CASES["slide"]
+    m = F.ball_model(theta, mu, iterations=50)
+    (q1, v1, _), (q2, v2, _) = _ball_gpu(m, [100, 500])
+    acc = (v2[0] - v1[0]) / (400 * m.timestep)
+    th = np.radians(theta)
+    np.testing.assert_allclose(acc, F.G * (np.sin(th) - mu * np.cos(th)), rtol=5e-3)
+    assert F._slip(q2, v2)[0] > 0.3 * v2[0]
+
+
+def test_kernel_impratio_scales_the_creep(require_gpu):
+    theta, mu = F.CASES["roll"]
+    creep = {}
+    for ir in (1.0, 10.0):
+        m = F.ball_model(theta, mu)
+        m.impratio = ir
+        (q, v, _), = _ball_gpu(m, [150])
+        creep[ir] = F._slip(q, v)[0]
+    assert creep[1.0] > 0 and creep[10.0] > 0
+    assert 5.0 < creep[1.0] / creep[10.0] < 15.0, creep

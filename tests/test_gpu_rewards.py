@@ -82,7 +82,7 @@ def _rollout_parity(env, keys, steps, seed, name, prep=None, max_frac=0.01):
         if prep is not None:  # edit the info, then re-read so the oracle starts from the edited record
             prep(t, st)
             env._write_state(st)
-            st = env._read_state(False)
+            st = env._issue(False)
         a = rs.uniform(-1, 1, size=(n, 12)).astype(np.float32)
         prev = st
         st = env.step(prev, a)
@@ -112,7 +112,9 @@ def test_all_reward_scales_one(model_path):
 
     def prep(t, st):
         # zero command on a third of the envs: the stand_still terms are active there
-        st.info["command"][::3] = 0.0
+        c = st.info["command"].copy()  # (State arrays are read-only, like the reference's jax arrays)
+        c[::3] = 0.0
+        st.info["command"] = c
 
     try:
         stats = _rollout_parity(e, make_keys(22, N), 30, 4, "reward_terms_scales_one", prep=prep)
@@ -132,11 +134,11 @@ def test_resample_branch_shared_cmd_rng(model_path):
     e = _make(model_path, resample_velocity_step=rvs)
     try:
         st = e.reset(make_keys(31, N))
-        st.info["step"][:] = np.where(np.arange(N) % 2 == 0, rvs, rvs - 1)
+        st.info["step"] = np.where(np.arange(N) % 2 == 0, rvs, rvs - 1).astype(st.info["step"].dtype)
         old_cmd = st.info["command"].copy()
         a = np.random.RandomState(5).uniform(-1, 1, size=(N, 12)).astype(np.float32)
         e._write_state(st)
-        prev = e._read_state(False)
+        prev = e._issue(False)
         out = e.step(prev, a)
         oe = O.OracleEnv(e.sys_model.struct, e.config_struct, precision="f32")
         for i in range(N):
@@ -166,7 +168,7 @@ def _tilted_state(e, keys, steps_info):
     q[:, 3:7] = [np.cos(np.pi / 4), np.sin(np.pi / 4), 0, 0]  # rolled 90 deg: done by tilt (:384-385)
     st.pipeline_state.q = q
     st.pipeline_state.qd = np.zeros_like(st.pipeline_state.qd)
-    st.info["step"][:] = steps_info
+    st.info["step"] = (np.zeros_like(st.info["step"]) + steps_info).astype(st.info["step"].dtype)
     return st
 
 
@@ -180,7 +182,7 @@ def test_termination_gate(model_path):
         st = _tilted_state(e, make_keys(41, N), steps)
         a = np.zeros((N, 12), np.float32)
         e._write_state(st)
-        prev = e._read_state(False)
+        prev = e._issue(False)
         out = e.step(prev, a)
         oe = O.OracleEnv(e.sys_model.struct, e.config_struct, precision="f32")
         it = 1 + _abi.REWARD_NAMES.index("termination")
