@@ -394,6 +394,10 @@ int pp3_field(pp3_env_t* env, int32_t field, void** dev_ptr, int64_t* elems_per_
 int pp3_copy_field_to_host(pp3_env_t* env, int32_t field, void* host, size_t bytes);
 int pp3_copy_field_from_host(pp3_env_t* env, int32_t field, const void* host, size_t bytes);
 int pp3_synchronize(pp3_env_t* env);
+/* Asynchronous device -> host copy of a whole field on the handle's stream (no synchronisation:
+ * pair it with pp3_synchronize).  Meant for page-locked host memory (pp3_host_malloc), which is
+ * what lets it run at PCIe speed without a staging copy (the host API's per-step outputs). */
+int pp3_copy_field_to_host_async(pp3_env_t* env, int32_t field, void* host, size_t bytes);
 /* The handle's own HIP stream (hipStream_t), for ordering other work (e.g. pp3_policy_act) with it. */
 void* pp3_stream(pp3_env_t* env);
 
@@ -403,6 +407,11 @@ int pp3_device_free(void* ptr);
 int pp3_memcpy_h2d(void* dst_dev, const void* src_host, size_t bytes);
 int pp3_memcpy_d2h(void* dst_host, const void* src_dev, size_t bytes);
 int pp3_memcpy_d2d(void* dst_dev, const void* src_dev, size_t bytes, void* stream);
+/* Asynchronous host -> device copy on `stream` (from page-locked memory: the host API's actions). */
+int pp3_memcpy_h2d_async(void* dst_dev, const void* src_host, size_t bytes, void* stream);
+/* Page-locked host memory (hipHostMalloc) for the host API's output arrays. */
+int pp3_host_malloc(size_t bytes, void** out);
+int pp3_host_free(void* ptr);
 
 /* Benchmark helpers: fill actions f32[N][12] with U(lo,hi) from a counter hash
  * keyed by (seed, step) on device; record HIP events around the step kernel

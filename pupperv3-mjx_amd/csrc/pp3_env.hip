@@ -3405,6 +3405,33 @@ int pp3_synchronize(pp3_env_t* e) {
   return PP3_OK;
 }
 
+int pp3_copy_field_to_host_async(pp3_env_t* e, int32_t field, void* host, size_t bytes) {
+  void* p;
+  int64_t n;
+  int rc = pp3_field(e, field, &p, &n);
+  if (rc) return rc;
+  if (bytes != (size_t)n * e->N * 4) return set_err(PP3_ERR_ARG, "pp3_copy_field_to_host_async: size mismatch");
+  if (!p) return set_err(PP3_ERR_ARG, "pp3_copy_field_to_host_async: field not allocated");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipMemcpyAsync(host, p, bytes, hipMemcpyDeviceToHost, e->stream));
+  return PP3_OK;
+}
+
+int pp3_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return PP3_OK;
+}
+
+int pp3_host_malloc(size_t bytes, void** out) {
+  if (!out) return set_err(PP3_ERR_ARG, "pp3_host_malloc: null output");
+  HIPCHK(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  return PP3_OK;
+}
+int pp3_host_free(void* p) {
+  HIPCHK(hipHostFree(p));
+  return PP3_OK;
+}
+
 int pp3_device_malloc(int32_t device, size_t bytes, void** out) {
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipMalloc(out, bytes));

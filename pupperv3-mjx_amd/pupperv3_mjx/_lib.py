@@ -51,6 +51,10 @@ def load() -> C.CDLL:
     L.pp3_copy_field_to_host.argtypes = [vp, i32, vp, sz]
     L.pp3_copy_field_from_host.argtypes = [vp, i32, vp, sz]
     L.pp3_synchronize.argtypes = [vp]
+    L.pp3_copy_field_to_host_async.argtypes = [vp, i32, vp, sz]
+    L.pp3_host_malloc.argtypes = [sz, C.POINTER(vp)]
+    L.pp3_memcpy_h2d_async.argtypes = [vp, vp, sz, vp]
+    L.pp3_host_free.argtypes = [vp]
     L.pp3_device_malloc.argtypes = [i32, sz, C.POINTER(vp)]
     L.pp3_device_free.argtypes = [vp]
     L.pp3_memcpy_h2d.argtypes = [vp, vp, sz]
@@ -88,7 +92,9 @@ def load() -> C.CDLL:
     L.pp3_comm_barrier.argtypes = [vp]
     for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
-                 "pp3_synchronize", "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
+                 "pp3_synchronize", "pp3_copy_field_to_host_async", "pp3_host_malloc", "pp3_host_free",
+                 "pp3_memcpy_h2d_async",
+                 "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
                  "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
                  "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy",
                  "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
@@ -118,6 +124,7 @@ EXPORTED_SYMBOLS = (
     "pp3_abi_version", "pp3_struct_size", "pp3_last_error", "pp3_device_count", "pp3_create", "pp3_destroy",
     "pp3_num_envs", "pp3_state_stride", "pp3_env_device", "pp3_reset", "pp3_step", "pp3_set_dr",
     "pp3_set_pipeline_output", "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
+    "pp3_copy_field_to_host_async", "pp3_host_malloc", "pp3_host_free", "pp3_memcpy_h2d_async",
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
     "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
@@ -126,6 +133,46 @@ EXPORTED_SYMBOLS = (
     "pp3_comm_last_error", "pp3_gather", "pp3_comm_allreduce", "pp3_comm_barrier",
     "pp3_render", "pp3_render_last_error",
 )
+
+
+class PinnedBlock:
+    """Page-locked host memory (pp3_host_malloc) exposed to numpy through __array_interface__:
+    arrays made from it keep it alive, and when the last one dies the block goes back to `pool`
+    (or is freed), so host-API output arrays never alias a block that a later step reuses."""
+
+    def __init__(self, nbytes: int, pool=None):
+        self.ptr = C.c_void_p()
+        self.nbytes = int(nbytes)
+        check(load().pp3_host_malloc(max(self.nbytes, 4), C.byref(self.ptr)))
+        self.__array_interface__ = {"shape": (self.nbytes // 4,), "typestr": "<f4", "version": 3,
+                                    "data": (self.ptr.value, False)}
+        self._pool = pool
+
+    @staticmethod
+    def take(nbytes: int, pool: list) -> "PinnedBlock":
+        """A block from `pool` (a list of free blocks) or a new one; it returns there when released."""
+        import weakref
+        b = pool.pop() if pool else PinnedBlock(nbytes, pool)
+        holder = _BlockRef(b)
+        weakref.finalize(holder, pool.append, b)
+        return holder
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                load().pp3_host_free(self.ptr)
+        except Exception:
+            pass
+
+
+class _BlockRef:
+    """One lease of a PinnedBlock: numpy arrays made from it reference this object, whose death
+    returns the block to its pool."""
+
+    def __init__(self, block: PinnedBlock):
+        self.block = block
+        self.ptr = block.ptr
+        self.__array_interface__ = block.__array_interface__
 
 
 class DeviceBuffer:

@@ -330,6 +330,9 @@ class PupperV3Env:
         self._gen = 0
         self._issued = None
         self._snap_pool = []
+        self._pin_pool = []    # page-locked output blocks (obs | reward | done) of issued states
+        self._act_stage = _lib.PinnedBlock(self.num_envs * _abi.NU * 4)  # page-locked action staging
+        self._act_stage_arr = np.asarray(self._act_stage)
         self._lazy_extra = {}  # field id -> info hook (wrappers.AutoResetEpisodeEnv: the episode record)
         self._field_elems = {f: self.device_field(f)[1] for f in (_abi.F_STATE, _abi.F_METRICS, _abi.F_PIPELINE)}
         self._field_elems[_abi.F_EPISODE] = _abi.EP_STRIDE
@@ -512,7 +515,10 @@ class PupperV3Env:
         act = np.ascontiguousarray(np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU))
         if not self.holds(state):
             self._write_state(state)
-        self._act_buf.upload(act)
+        # actions through a page-locked staging block, copied on the env's stream ahead of the launch
+        np.copyto(self._act_stage_arr, act.reshape(-1))
+        _lib.check(self._L.pp3_memcpy_h2d_async(self._act_buf.ptr, self._act_stage.ptr, act.nbytes,
+                                                 self._L.pp3_stream(self._h)))
         self.step_device(self._act_buf.ptr.value)
         return self._issue(single)
 
@@ -536,10 +542,19 @@ class PupperV3Env:
         return out
 
     def _issue(self, single: bool) -> DeviceState:
+        # obs | reward | done land in one page-locked block (async copies on the env's stream, one
+        # sync); the arrays are views of it and keep it leased until the last of them dies
+        n, D = self.num_envs, self.observation_size
+        lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
+        base = lease.ptr.value
+        for f, off, nb in ((_abi.F_OBS, 0, 4 * n * D), (_abi.F_REWARD, 4 * n * D, 4 * n),
+                           (_abi.F_DONE, 4 * n * (D + 1), 4 * n)):
+            _lib.check(self._L.pp3_copy_field_to_host_async(self._h, f, C.c_void_p(base + off), nb))
         self.synchronize()
-        obs = _ro(self._get(_abi.F_OBS))
-        rew = _ro(self._get(_abi.F_REWARD)[:, 0])
-        done = _ro(self._get(_abi.F_DONE)[:, 0])
+        flat = np.asarray(lease)
+        obs = _ro(flat[:n * D].reshape(n, D))
+        rew = _ro(flat[n * D:n * (D + 1)])
+        done = _ro(flat[n * (D + 1):])
         if single:
             obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
         st = DeviceState(self, self._gen, single, obs, rew, done)

@@ -93,7 +93,9 @@ def test_kernel_converged_qacc_equals_documented_soft_pyramid(require_gpu, case)
         e.close()
     a, info = F.ball_qacc(m, q, v)
     assert info["dist"] < 0 and sum(info["active"]) >= 1
-    np.testing.assert_allclose(w2[0, 0:6], a, atol=2e-3 * F.G + 2e-3 * np.abs(a))
+    err = np.abs(w2[0, 0:6] - a)
+    assert np.all(err <= 2e-3 * F.G + 2e-3 * np.abs(a)), (w2[0, 0:6], a)
+    G.report(f"friction_kat_converged_{case}", {"qacc_abs_err_max": float(err.max()), "qacc": a.tolist()})
 
 
 def test_kernel_ball_rolls_at_five_sevenths_g_sin(require_gpu):
