@@ -44,6 +44,8 @@ def lib(precision: str = "f64") -> C.CDLL:
         L.orc_choice.restype = C.c_int
         L.orc_set_partitionable.argtypes = [C.c_int]
         L.orc_set_ncon_max.argtypes = [C.c_int]
+        L.orc_set_ls_noise.argtypes = [C.c_int]
+        L.orc_ls_take.argtypes = [C.POINTER(C.c_long)]
         L.orc_data_size.restype = C.c_size_t
         L.orc_boundary_take.restype = C.c_int
         _LIBS[name] = L

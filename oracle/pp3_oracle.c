@@ -27,6 +27,7 @@
  * independent, specialised implementation checked against it.
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -42,6 +43,7 @@
 typedef REAL real;
 
 #if defined(ORC_FLOAT)
+#define REPS ((real)1.1920929e-7)  /* FLT_EPSILON */
 #define RSQRT sqrtf
 #define RCOS cosf
 #define RSIN sinf
@@ -49,6 +51,7 @@ typedef REAL real;
 #define RFABS fabsf
 #define RPOW powf
 #else
+#define REPS ((real)2.220446049250313e-16)  /* DBL_EPSILON */
 #define RSQRT sqrt
 #define RCOS cos
 #define RSIN sin
@@ -955,9 +958,23 @@ typedef struct {
   int evals;
 } LSCtx;
 
+static int g_ls_trace = 0;
 static void ls_eval(LSCtx* c, LSPoint* p) {
   const Data* d = c->d;
   real a = p->alpha;
+  if (g_ls_trace) {
+    static char prev[ORC_MAXEFC];
+    int nch = 0;
+    for (int r = 0; r < d->nefc; r++) {
+      real x = c->Jaref[r] + a * c->Jv[r];
+      char st;
+      if (d->efc_type[r] == CN_FRICTION) { real rf = d->efc_R[r] * d->efc_floss[r]; st = x <= -rf ? 1 : (x >= rf ? 2 : 0); }
+      else st = x >= 0 ? 3 : 0;
+      if (c->evals > 0 && st != prev[r]) nch++;
+      prev[r] = st;
+    }
+    printf("  eval %d alpha %.9g changed %d\n", c->evals, (double)a, nch);
+  }
   real t0 = c->quadG[0], t1 = c->quadG[1], t2 = c->quadG[2];
   for (int r = 0; r < d->nefc; r++) {
     real jar = c->Jaref[r], jv = c->Jv[r], D = d->efc_D[r];
@@ -980,6 +997,21 @@ static void ls_eval(LSCtx* c, LSPoint* p) {
   c->evals++;
 }
 
+/* Line-search convergence: MuJoCo's |derivative| < gtol, or -- the arithmetic's floor -- the
+ * remaining Newton correction |d0 / d1| at or below LS_NOISE roundoffs of alpha in the precision
+ * of `real` (a derivative that small is rounding noise: below it the search only moves alpha by
+ * noise).  In double this floor sits ~1e-14 relative, far below any gtol MuJoCo's tolerances give,
+ * so the fp64 oracle is PrimalSearch unchanged; in float it stops the search where MuJoCo in
+ * double stops (a Newton step that landed on the 1-D minimum) instead of spending the remaining
+ * ls_iterations on noise.  The HIP kernel applies the same rule with FLT_EPSILON. */
+#define LS_NOISE ((real)64)
+static int g_ls_noise = 1;
+static _Thread_local long g_ls_total = 0, g_ls_calls = 0;  /* line-search evaluations / searches (diagnostics) */
+static int ls_converged(const LSPoint* p, real gtol) {
+  if (RFABS(p->d0) < gtol) return 1;
+  return g_ls_noise && RFABS(p->d0) <= LS_NOISE * REPS * p->d1 * RFABS(p->alpha);
+}
+
 /* engine_solver.c PrimalSearch-style exact line search: Newton step from 0, one-sided Newton
  * until the derivative changes sign, then bracketed Newton/midpoint refinement. */
 static real line_search(LSCtx* c, real gtol, int maxit) {
@@ -989,14 +1021,14 @@ static real line_search(LSCtx* c, real gtol, int maxit) {
   p1.alpha = p0.alpha - p0.d0 / p0.d1;
   ls_eval(c, &p1);
   if (p0.cost < p1.cost) p1 = p0;
-  if (RFABS(p1.d0) < gtol) return p1.alpha;
+  if (ls_converged(&p1, gtol)) return p1.alpha;
   real dir = p1.d0 < 0 ? 1 : -1;
   p2 = p1;
   while (p1.d0 * dir <= -gtol && c->evals < maxit) {
     p2 = p1;
     p1.alpha -= p1.d0 / p1.d1;
     ls_eval(c, &p1);
-    if (RFABS(p1.d0) < gtol) return p1.alpha;
+    if (ls_converged(&p1, gtol)) return p1.alpha;
   }
   if (c->evals >= maxit) return p1.alpha;
   /* bracket [p2, p1]: p2.d0*dir < 0 < p1.d0*dir */
@@ -1009,7 +1041,7 @@ static real line_search(LSCtx* c, real gtol, int maxit) {
     LSPoint cand[3] = {p1n, p2n, pmid};
     int best = -1;
     for (int i = 0; i < 3; i++)
-      if (RFABS(cand[i].d0) < gtol && (best < 0 || cand[i].cost < cand[best].cost)) best = i;
+      if (ls_converged(&cand[i], gtol) && (best < 0 || cand[i].cost < cand[best].cost)) best = i;
     if (best >= 0) return cand[best].alpha;
     int up1 = 0, up2 = 0;
     for (int i = 0; i < 3; i++) {
@@ -1119,12 +1151,15 @@ static void solve_newton(const Model* m, Data* d) {
     }
     real gtol = m->tolerance * m->ls_tolerance * snorm / scale;
     real alpha = line_search(&c, gtol, m->ls_iterations);
+    if (g_ls_trace) printf(" -> alpha %.9g evals %d nefc %d gtol %.3g\n", (double)alpha, c.evals, nefc, (double)gtol);
     /* debug record of the last Newton iteration (orc_debug_read) */
     for (int i = 0; i < NV; i++) { g_dbg[i] = (double)qacc[i]; g_dbg[18 + i] = (double)grad[i]; g_dbg[36 + i] = (double)search[i]; }
     g_dbg[54] = (double)c.quadG[0]; g_dbg[55] = (double)c.quadG[1]; g_dbg[56] = (double)c.quadG[2];
     g_dbg[57] = (double)snorm; g_dbg[58] = (double)gtol; g_dbg[59] = (double)alpha; g_dbg[60] = (double)c.evals;
     g_dbg[61] = (double)cost_ws; g_dbg[62] = (double)cost_sm; g_dbg[63] = (double)nefc;
     d->ls_evals += c.evals;
+    g_ls_total += c.evals;
+    g_ls_calls++;
     if (alpha == 0) break;
     for (int i = 0; i < NV; i++) qacc[i] += alpha * search[i];
     (void)cost;
@@ -1717,6 +1752,10 @@ int orc_env_rollout(const pp3_model_t* mm, const pp3_env_config_t* cfg, int n, i
 }
 
 void orc_set_ncon_max(int n) { g_ncon_max = n; }
+void orc_set_ls_noise(int on) { g_ls_noise = on; }
+void orc_set_ls_trace(int on) { g_ls_trace = on; }
+/* line-search evaluations and searches of this thread since the last call */
+void orc_ls_take(long* out) { out[0] = g_ls_total; out[1] = g_ls_calls; g_ls_total = 0; g_ls_calls = 0; }
 void orc_debug_read(double* out) { memcpy(out, g_dbg, sizeof(g_dbg)); }
 int orc_boundary_take(void) { const int n = g_boundary; g_boundary = 0; return n; }
 

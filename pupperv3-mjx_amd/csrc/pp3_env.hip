@@ -16,6 +16,7 @@
 // pivot column broadcast through LDS; half-wave reductions run on the DPP network.
 #include <hip/hip_runtime.h>
 
+#include <float.h>
 #include <math.h>
 #include <stddef.h>
 #include <stdio.h>
@@ -38,6 +39,7 @@ constexpr int HMAX = 16;    // observation_history limit
 constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + HW - 1) / HW;
 constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
 constexpr int NHIT = 64;        // contact-overflow ranking window (hits kept for ranking)
+constexpr float LS_NOISE = 64.0f;  // line-search convergence floor, in roundoffs of alpha (oracle LS_NOISE)
 
 // Phase-local scratch that never lives across a phase boundary it does not own.
 template <int NC>
@@ -144,6 +146,7 @@ __device__ __forceinline__ LaneRec<N> fetch_rec(const LaneTab<N>& t, int l) {
 __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float dpp_shr4(float v) { return dpp_f<0x114, 0xF>(v, v); }  // lane i <- i-4 (row)
 
 // wave priority by load (env_step_kernel): contact-weight thresholds (contacts of the busier env
 // of the wave, +2 on the leg-leg Newton path) for the upper priority pair / the top priority
@@ -197,27 +200,20 @@ template <int NC>
 __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l, bool euler) {
   // every model constant of the phase is fetched up front (clamped lane indices, no branches)
   // and pinned by one asm statement: one vmcnt wait instead of one per dependent use
+  // lane l < 12 owns leg body (level kl = l / 4, leg gl = l % 4): body bl, joint jl, qpos ql
   const int lc = l < 12 ? l : 11, gl = lc & 3, kl = lc >> 2;
   const int bl = 2 + 3 * gl + kl, jl = 1 + 3 * gl + kl, ql = 7 + 3 * gl + kl;
-  float jax[3], bq[4], q0, bpos[3][3], jaxc[3][3];
+  float jax[3], bq[4], q0, bpos[3], cpos[3];
   for (int c = 0; c < 3; c++) jax[c] = m.jnt_axis[jl][c];
   for (int c = 0; c < 4; c++) bq[c] = m.body_quat[bl][c];
   q0 = m.qpos0[ql];
-  {
-    const int g4 = l & 3;
 #pragma unroll
-    for (int k = 0; k < 3; k++)
-#pragma unroll
-      for (int c = 0; c < 3; c++) {
-        bpos[k][c] = m.body_pos[2 + 3 * g4 + k][c];
-        jaxc[k][c] = m.jnt_axis[1 + 3 * g4 + k][c];
-      }
+  for (int c = 0; c < 3; c++) {
+    bpos[c] = m.body_pos[bl][c];                    // this body's offset in its parent
+    cpos[c] = m.body_pos[kl < 2 ? bl + 1 : bl][c];  // its child's offset in it (levels 0, 1)
   }
   PIN("+v"(jax[0]), "+v"(jax[1]), "+v"(jax[2]), "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(q0),
-      "+v"(bpos[0][0]), "+v"(bpos[0][1]), "+v"(bpos[0][2]), "+v"(bpos[1][0]), "+v"(bpos[1][1]),
-      "+v"(bpos[1][2]), "+v"(bpos[2][0]), "+v"(bpos[2][1]), "+v"(bpos[2][2]), "+v"(jaxc[0][0]),
-      "+v"(jaxc[0][1]), "+v"(jaxc[0][2]), "+v"(jaxc[1][0]), "+v"(jaxc[1][1]), "+v"(jaxc[1][2]),
-      "+v"(jaxc[2][0]), "+v"(jaxc[2][1]), "+v"(jaxc[2][2]));
+      "+v"(bpos[0]), "+v"(bpos[1]), "+v"(bpos[2]), "+v"(cpos[0]), "+v"(cpos[1]), "+v"(cpos[2]));
   // The previous substep's Euler step (eulerdamp disabled), deferred to here when `euler`: the
   // joint lanes integrate their own dof (so the new angle stays in a register), lanes 12..17 the
   // base dofs, and lane 15 integrates the base quaternion -- its axis-angle rotation shares the
@@ -255,51 +251,78 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
       for (int k = 0; k < 4; k++) s.qpos[3 + k] = qb[k];
     }
   }
-  SYNC();  // the base position / quaternion stores above precede the chain lanes' reads below
-  // the 3 levels of this lane's leg (lanes 0..3 consume); width-32 shuffles stay in the half
-  float lq1[4], lq2[4];
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    lq1[c] = __shfl(lq[c], (l & 3) + 4, HW);
-    lq2[c] = __shfl(lq[c], (l & 3) + 8, HW);
+  SYNC();  // the base position / quaternion stores above precede the reads below
+  float pq[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
+  normalize4(pq);
+  const float pp[3] = {s.qpos[0], s.qpos[1], s.qpos[2]};
+  float pR[9];
+  quat2mat(pq, pR);
+  if (l == 0) {
+    float off[3];
+    matvec(off, pR, s.ipos[1]);
+    for (int c = 0; c < 3; c++) {
+      s.xpos[1][c] = pp[c];
+      s.x.xipos[1][c] = pp[c] + off[c];
+      s.xaxis[0][c] = m.jnt_axis[0][c];
+    }
+    for (int c = 0; c < 4; c++) s.xquat[1][c] = pq[c];
   }
-  if (l < 4) {
-    float pq[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
-    normalize4(pq);
-    float pp[3] = {s.qpos[0], s.qpos[1], s.qpos[2]};
-    float pR[9];
-    quat2mat(pq, pR);
-    if (l == 0) {
-      float off[3];
-      matvec(off, pR, s.ipos[1]);
-      for (int c = 0; c < 3; c++) {
-        s.xpos[1][c] = pp[c];
-        s.x.xipos[1][c] = pp[c] + off[c];
-        s.xaxis[0][c] = m.jnt_axis[0][c];
-      }
-      for (int c = 0; c < 4; c++) s.xquat[1][c] = pq[c];
-    }
+  // The 12 leg bodies on their own lanes: lane l = 4 level + leg, so a body's parent (level - 1,
+  // same leg) is lane l - 4 of the same 16-lane DPP row and each level's frame reaches the next
+  // by one row_shr:4.  Same arithmetic as walking each chain on one lane (mj_kinematics:
+  // xquat_k = normalize(xquat_{k-1} lq_k), xpos_k = xpos_{k-1} + R_{k-1} bpos_k), but only the
+  // quaternion composition and the position sums are serial across levels: every rotation matrix,
+  // child offset, axis and COM is computed by its body's lane at once.
+  // (every DPP source is pinned on all lanes first: otherwise the compiler may compute it, and
+  // run the DPP, only on the lanes that consume the result -- which are not the source lanes)
+  float xq[4];
+  mulquat(xq, pq, lq);
+  normalize4(xq);  // level 0 final
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int b = 2 + 3 * l + k, j = 1 + 3 * l + k;
-      const float* lqk = k == 0 ? lq : (k == 1 ? lq1 : lq2);
-      float xp[3], xq[4], off[3], R[9], ax[3];
-      matvec(off, pR, bpos[k]);
-      for (int c = 0; c < 3; c++) xp[c] = pp[c] + off[c];
-      mulquat(xq, pq, lqk);
-      normalize4(xq);
-      quat2mat(xq, R);
-      matvec(ax, R, jaxc[k]);
-      matvec(off, R, s.ipos[b]);
-      for (int c = 0; c < 3; c++) {
-        s.xpos[b][c] = xp[c];
-        s.x.xipos[b][c] = xp[c] + off[c];
-        s.xaxis[j][c] = ax[c];
-        pp[c] = xp[c];
-      }
-      for (int c = 0; c < 4; c++) { s.xquat[b][c] = xq[c]; pq[c] = xq[c]; }
-      for (int c = 0; c < 9; c++) pR[c] = R[c];
+  for (int lev = 1; lev < 3; lev++) {
+    float par[4], t[4];
+    PIN("+v"(xq[0]), "+v"(xq[1]), "+v"(xq[2]), "+v"(xq[3]));
+#pragma unroll
+    for (int c = 0; c < 4; c++) par[c] = dpp_shr4(xq[c]);
+    PIN("+v"(par[0]), "+v"(par[1]), "+v"(par[2]), "+v"(par[3]));
+    mulquat(t, par, lq);
+    normalize4(t);
+#pragma unroll
+    for (int c = 0; c < 4; c++) xq[c] = kl >= lev ? t[c] : xq[c];  // level lev final
+  }
+  float R[9], ob[3], co[3], o[3], xp[3];
+  quat2mat(xq, R);
+  matvec(ob, pR, bpos);  // level 0: R_base bpos
+  matvec(co, R, cpos);   // this body's child offset R_k bpos_{k+1}
+  PIN("+v"(co[0]), "+v"(co[1]), "+v"(co[2]));
+  float sh[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) sh[c] = dpp_shr4(co[c]);
+  PIN("+v"(sh[0]), "+v"(sh[1]), "+v"(sh[2]));
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    o[c] = kl == 0 ? ob[c] : sh[c];  // R_{k-1} bpos_k
+    xp[c] = pp[c] + o[c];            // level 0 final
+  }
+#pragma unroll
+  for (int lev = 1; lev < 3; lev++) {
+    PIN("+v"(xp[0]), "+v"(xp[1]), "+v"(xp[2]));
+#pragma unroll
+    for (int c = 0; c < 3; c++) sh[c] = dpp_shr4(xp[c]);
+    PIN("+v"(sh[0]), "+v"(sh[1]), "+v"(sh[2]));
+#pragma unroll
+    for (int c = 0; c < 3; c++) xp[c] = kl >= lev ? sh[c] + o[c] : xp[c];  // level lev final
+  }
+  if (l < 12) {
+    float ax[3], off[3];
+    matvec(ax, R, jax);
+    matvec(off, R, s.ipos[bl]);
+    for (int c = 0; c < 3; c++) {
+      s.xpos[bl][c] = xp[c];
+      s.x.xipos[bl][c] = xp[c] + off[c];
+      s.xaxis[jl][c] = ax[c];
     }
+    for (int c = 0; c < 4; c++) s.xquat[bl][c] = xq[c];
   }
 }
 
@@ -1636,14 +1659,9 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       q2 = 0.5f * sv * mv;
       sn = sv * sv;
     }
-    q1 = hsum(q1, h);
-    q2 = hsum(q2, h);
-    sn = sqrtf(hsum(sn, h));
-    live = live && !(sn < MINVAL);
     float jv[NR];
 #pragma unroll
     for (int t = 0; t < NR; t++) jv[t] = valid[t] ? row_dot(s, l + HW * t, nl, ncon, s.search) : 0.0f;
-    const float gtol = m.gtol_scale * sn;
     // Each row's cost on the line qacc + alpha*search is piecewise quadratic in alpha: the three
     // pieces' coefficients (below the lower switch point, above the upper one, in between) are
     // alpha-independent and computed once here; an evaluation only picks the piece per row.
@@ -1670,6 +1688,11 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
 #ifdef PP3_PHASE_PROF
     if (pf && NR > 1 && rowany[NR - 1]) pf->slot2++;
 #endif
+    q1 = hsum(q1, h);
+    q2 = hsum(q2, h);
+    sn = sqrtf(hsum(sn, h));
+    live = live && !(sn < MINVAL);
+    const float gtol = m.gtol_scale * sn;
     // cost and derivatives of the 1-D piecewise quadratic at alpha (alpha is per half)
     auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
       float t0 = 0, t1 = 0, t2 = 0;
@@ -1689,6 +1712,12 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       d0 = t1 + 2.0f * alpha * t2;
       d1 = fmaxf(2.0f * t2, MINVAL);
     };
+    // converged at (alpha, d0, d1): MuJoCo's |d0| < gtol, or the remaining Newton correction
+    // |d0 / d1| within LS_NOISE roundoffs of alpha -- the fp32 floor below which the search would
+    // only move alpha by rounding noise (the oracle's ls_converged, FLT_EPSILON in its float build)
+    auto conv = [&](float a, float d0, float d1) {
+      return fabsf(d0) < gtol || fabsf(d0) <= LS_NOISE * FLT_EPSILON * d1 * fabsf(a);
+    };
     // PrimalSearch-style exact line search (same control flow as the oracle); every branch
     // below is per env (per half), the wave runs the union of both envs' evaluations
     float alpha = 0.0f;
@@ -1702,7 +1731,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       eval(a1, c1, g1, h1);
       evals++;
       if (c0 < c1) { a1 = 0.0f; c1 = c0; g1 = g0; h1 = h0; }
-      if (fabsf(g1) < gtol) {
+      if (conv(a1, g1, h1)) {
         alpha = a1;
       } else {
         const float dir = g1 < 0 ? 1.0f : -1.0f;
@@ -1713,7 +1742,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
           a1 = a1 - g1 / h1;
           eval(a1, c1, g1, h1);
           evals++;
-          if (fabsf(g1) < gtol) { done = true; break; }
+          if (conv(a1, g1, h1)) { done = true; break; }
         }
         if (done || evals >= maxit) {
           alpha = a1;
@@ -1731,7 +1760,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
             eval(am, cm, gm, hm);
             evals++;
             // converged candidate with the lowest cost (order: p1next, p2next, mid)
-            bool ok0 = fabsf(g1n) < gtol, ok1 = fabsf(g2n) < gtol, ok2 = fabsf(gm) < gtol;
+            bool ok0 = conv(a1n, g1n, h1n), ok1 = conv(a2n, g2n, h2n), ok2 = conv(am, gm, hm);
             if (ok0 || ok1 || ok2) {
               float ba = ok0 ? a1n : (ok1 ? a2n : am), bc = ok0 ? c1n : (ok1 ? c2n : cm);
               if (ok1 && c2n < bc) { ba = a2n; bc = c2n; }
