@@ -1006,7 +1006,7 @@ static void ls_eval(LSCtx* c, LSPoint* p) {
  * ls_iterations on noise.  The HIP kernel applies the same rule with FLT_EPSILON. */
 #define LS_NOISE ((real)64)
 static int g_ls_noise = 1;
-static _Thread_local long g_ls_total = 0, g_ls_calls = 0;  /* line-search evaluations / searches (diagnostics) */
+static _Thread_local long g_ls_total = 0, g_ls_calls = 0, g_ls_smooth = 0, g_ls_starts = 0;  /* line-search evaluations / searches (diagnostics) */
 static int ls_converged(const LSPoint* p, real gtol) {
   if (RFABS(p->d0) < gtol) return 1;
   return g_ls_noise && RFABS(p->d0) <= LS_NOISE * REPS * p->d1 * RFABS(p->alpha);
@@ -1072,6 +1072,8 @@ static void solve_newton(const Model* m, Data* d) {
   for (int i = 0; i < NV; i++) cost_ws += (real)0.5 * (Ma[i] - d->qfrc_smooth[i]) * (d->qacc_warmstart[i] - d->qacc_smooth[i]);
   real cost_sm = constraint_update(d, jar_s, 0);
   if (RFABS(cost_ws - cost_sm) < BOUNDARY_REL * (RFABS(cost_ws) + RFABS(cost_sm))) g_boundary++;
+  g_ls_smooth += cost_ws > cost_sm;
+  g_ls_starts++;
   if (cost_ws > cost_sm) memcpy(qacc, d->qacc_smooth, sizeof(qacc));
   else memcpy(qacc, d->qacc_warmstart, sizeof(qacc));
 
@@ -1755,7 +1757,10 @@ void orc_set_ncon_max(int n) { g_ncon_max = n; }
 void orc_set_ls_noise(int on) { g_ls_noise = on; }
 void orc_set_ls_trace(int on) { g_ls_trace = on; }
 /* line-search evaluations and searches of this thread since the last call */
-void orc_ls_take(long* out) { out[0] = g_ls_total; out[1] = g_ls_calls; g_ls_total = 0; g_ls_calls = 0; }
+void orc_ls_take(long* out) {
+  out[0] = g_ls_total; out[1] = g_ls_calls; out[2] = g_ls_smooth; out[3] = g_ls_starts;
+  g_ls_total = 0; g_ls_calls = 0; g_ls_smooth = 0; g_ls_starts = 0;
+}
 void orc_debug_read(double* out) { memcpy(out, g_dbg, sizeof(g_dbg)); }
 int orc_boundary_take(void) { const int n = g_boundary; g_boundary = 0; return n; }
 

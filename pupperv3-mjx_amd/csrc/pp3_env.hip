@@ -1054,7 +1054,12 @@ __device__ __forceinline__ float ldl_arrow_solve_b(float (&a)[NV], float rhs, in
 template <int J0, int J1>
 __device__ __forceinline__ void hess_acc_p(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
 #pragma unroll
-  for (int j = J0; j < J1; j++) a[npos(j)] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
+  for (int j = J0; j < J1; j++) {  // three FMAs into the entry (not mul + 2 fma + add)
+    float v = a[npos(j)];
+    v = fmaf(w0, J[0][j], v);
+    v = fmaf(w1, J[1][j], v);
+    a[npos(j)] = fmaf(w2, J[2][j], v);
+  }
 }
 
 // (M x)[pnat(l)] from this lane's permuted M row held in registers (mrow[j] = M[pnat(l)][pnat(j)])
@@ -1168,7 +1173,7 @@ __device__ __forceinline__ void row_dot2(const Shared<NC>& s, int r, int nl, int
 template <int J0, int J1>
 __device__ __forceinline__ void hess_acc(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
 #pragma unroll
-  for (int j = J0; j < J1; j++) a[j] += w0 * J[0][j] + w1 * J[1][j] + w2 * J[2][j];
+  for (int j = J0; j < J1; j++) a[j] = fmaf(w2, J[2][j], fmaf(w1, J[1][j], fmaf(w0, J[0][j], a[j])));
 }
 
 // index drawn by jax.random.choice(p) from u = uniform(key): searchsorted_left(cumsum(p), cumsum[-1]*(1-u))
