@@ -216,10 +216,42 @@ def _orientation(attrs: Dict[str, str], angle_deg: bool) -> np.ndarray:
         v = _vec(attrs["axisangle"])
         ang = math.radians(v[3]) if angle_deg else v[3]
         return axis_angle_quat(v[:3], ang)
-    for key in ("euler", "xyaxes", "zaxis"):
-        if key in attrs:
-            raise NotImplementedError(f"MJCF orientation '{key}' is not used by the Pupper model")
+    if "xyaxes" in attrs:  # x axis, then y made orthogonal to it; z = x cross y (MJCF spec)
+        v = _vec(attrs["xyaxes"])
+        x = v[:3] / np.linalg.norm(v[:3])
+        y = v[3:6] - (v[3:6] @ x) * x
+        y = y / np.linalg.norm(y)
+        return _mat_to_quat(np.stack([x, y, np.cross(x, y)], axis=1))
+    if "zaxis" in attrs:  # the minimal rotation taking (0, 0, 1) to the given axis
+        z = _vec(attrs["zaxis"])
+        z = z / np.linalg.norm(z)
+        axis = np.cross([0.0, 0.0, 1.0], z)
+        s, c = np.linalg.norm(axis), z[2]
+        if s < 1e-12:
+            return np.array([1.0, 0, 0, 0]) if c > 0 else np.array([0.0, 1.0, 0, 0])
+        return axis_angle_quat(axis / s, math.atan2(s, c))
+    if "euler" in attrs:
+        raise NotImplementedError("MJCF orientation 'euler' is not used by the Pupper model")
     return np.array([1.0, 0, 0, 0])
+
+
+def _mat_to_quat(R: np.ndarray) -> np.ndarray:
+    """Unit quaternion (w, x, y, z) of a rotation matrix (columns = the frame's axes)."""
+    t = np.trace(R)
+    if t > 0:
+        w = math.sqrt(1.0 + t) / 2
+        q = [w, (R[2, 1] - R[1, 2]) / (4 * w), (R[0, 2] - R[2, 0]) / (4 * w), (R[1, 0] - R[0, 1]) / (4 * w)]
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        r = math.sqrt(max(1.0 + R[i, i] - R[j, j] - R[k, k], 1e-300))
+        q = [0.0, 0.0, 0.0, 0.0]
+        q[1 + i] = r / 2
+        q[0] = (R[k, j] - R[j, k]) / (2 * r)
+        q[1 + j] = (R[j, i] + R[i, j]) / (2 * r)
+        q[1 + k] = (R[k, i] + R[i, k]) / (2 * r)
+    q = np.array(q)
+    return q / np.linalg.norm(q)
 
 
 def _compile(root: ET.Element, xml: str) -> CompiledModel:
@@ -636,11 +668,16 @@ def _visual(root: ET.Element, geoms: List[dict], body_names: List[str], angle_de
                          group=g["group"], mesh=g["mesh"], material=g["material"], rgba=g["rgba"], name=g["name"])
                     for g in geoms]
     wb = root.find("worldbody")
+    parent_of = {child: parent for parent in wb.iter() for child in parent}
     for c in wb.iter("camera"):
+        par = parent_of.get(c, wb)
+        parent = 0 if par is wb else (body_names.index(par.get("name")) if par.get("name") in body_names else -1)
+        if parent < 0:
+            raise NotImplementedError("camera inside an unnamed body")
         vis["cameras"][c.get("name", f"camera{len(vis['cameras'])}")] = dict(
             mode=c.get("mode", "fixed"), target=body_names.index(c.get("target")) if c.get("target") in body_names else -1,
             pos=_vec(c.get("pos", "0 0 0"), 3), quat=_orientation(c.attrib, angle_deg),
-            fovy=float(c.get("fovy", "45")), parent_world=c in list(wb))
+            fovy=float(c.get("fovy", "45")), parent=parent)
     return vis
 
 

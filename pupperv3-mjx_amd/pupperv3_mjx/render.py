@@ -215,10 +215,34 @@ class Scene:
             out[i, 9:] = xpos[it["body"]] + Rb @ it["pos"]
         return out
 
+    def _frames(self, qpos):
+        """Body origins, rotations and subtree centres of mass at qpos (mj_kinematics, mj_comPos)."""
+        m = self.cm.struct
+        xpos, xquat, _, _ = mjcf._kinematics(m, np.asarray(qpos, np.float64))
+        R = np.array([mjcf.quat_to_mat(q) for q in xquat])
+        nb = len(xpos)
+        mass = np.array(m.body_mass[:nb], float)
+        xipos = np.array([xpos[b] + R[b] @ np.array(m.body_ipos[b][:]) for b in range(nb)])
+        com = np.zeros((nb, 3))
+        msum = np.zeros(nb)
+        for b in range(nb - 1, 0, -1):  # children have larger ids than their parents
+            com[b] += mass[b] * xipos[b]
+            msum[b] += mass[b]
+            p = m.body_parentid[b]
+            if p > 0:
+                com[p] += com[b]
+                msum[p] += msum[b]
+        subtree = np.where(msum[:, None] > 0, com / np.maximum(msum, 1e-300)[:, None], xipos)
+        return xpos, R, subtree
+
     def camera(self, name, qpos: np.ndarray, height: int) -> np.ndarray:
-        """[16]: position, right, up, forward, focal length in pixels (MuJoCo camera rules)."""
+        """[16]: position, right, up, forward, focal length in pixels, by MuJoCo's camera rules
+        (mj_camlight): the camera's pose is given in its parent body's frame; "fixed" moves with
+        that body, "track" / "trackcom" keep the world offset to the body / its subtree COM and the
+        world orientation they have at qpos0, "targetbody" / "targetbodycom" sit where "fixed" puts
+        them and look at the target body's origin / subtree COM."""
         vis = self.cm.visual
-        xpos, xquat, _, _ = mjcf._kinematics(self.cm.struct, np.asarray(qpos, np.float64))
+        xpos, R, subtree = self._frames(qpos)
         if name is None or (isinstance(name, int) and name < 0):  # MuJoCo's free camera: look at the base
             target = xpos[1]
             pos = target + np.array([0.0, -1.0, 0.6])
@@ -229,14 +253,28 @@ class Scene:
                 raise ValueError(f'The camera "{name}" does not exist.')
             cam = vis["cameras"][name]
             fovy = cam["fovy"]
-            pos = np.array(cam["pos"], float)
-            if cam["mode"] in ("targetbody", "targetbodycom") and cam["target"] >= 0:
-                z = pos - xpos[cam["target"]]
-            elif cam["mode"] in ("track", "trackcom"):
-                pos = xpos[1] + pos
-                z = mjcf.quat_to_mat(cam["quat"])[:, 2]
+            b = cam["parent"]
+            mode = cam["mode"]
+            lpos, lR = np.array(cam["pos"], float), mjcf.quat_to_mat(cam["quat"])
+            frame = None  # the camera frame's world axes, where the mode fixes them
+            if mode in ("track", "trackcom"):
+                x0, R0, c0 = self._frames(np.array(self.cm.struct.qpos0[:]))
+                anchor0 = (c0 if mode == "trackcom" else x0)[b]
+                anchor = (subtree if mode == "trackcom" else xpos)[b]
+                pos = anchor + (x0[b] + R0[b] @ lpos - anchor0)
+                frame = R0[b] @ lR
+            elif mode in ("fixed", "targetbody", "targetbodycom"):
+                pos = xpos[b] + R[b] @ lpos
+                frame = R[b] @ lR
+                if mode != "fixed" and cam["target"] >= 0:
+                    tgt = (subtree if mode == "targetbodycom" else xpos)[cam["target"]]
+                    frame = None
+                    z = pos - tgt
             else:
-                z = mjcf.quat_to_mat(cam["quat"])[:, 2]
+                raise NotImplementedError(f'camera mode "{mode}"')
+            if frame is not None:
+                fpx = 0.5 * height / math.tan(math.radians(fovy) / 2)
+                return np.concatenate([pos, frame[:, 0], frame[:, 1], -frame[:, 2], [fpx, 0, 0, 0]]).astype(np.float32)
         z = z / np.linalg.norm(z)
         x = np.cross([0.0, 0.0, 1.0], z)
         if np.linalg.norm(x) < 1e-9:

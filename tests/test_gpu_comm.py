@@ -3,11 +3,17 @@
 pp3_gather on a one-rank RCCL communicator: the device pack of obs | reward | done (with padding
 rows past the shard) must equal sharding.pack_rows of the env's own fields, for the gather to
 a root and for the all-gather; the reductions the bench's max-over-ranks timing uses must
-return their inputs.  (Several ranks need several GPUs -- RCCL allows one rank per device --
-so the N > 1 exchange itself is covered by the gloo test in test_sharding.py and the driver's
-8-GPU bench.)
+return their inputs.  Several ranks need several GPUs (RCCL allows one rank per device):
+test_two_rank_gather_on_two_devices runs the grouped send/recv and the all-gather across two
+processes when the box has two devices and is skipped otherwise; the N > 1 path also runs, with
+its checksum check, in every multi-GPU bench (bench.py gather_check).  Until one of those has run
+on hardware, the multi-rank exchange is unverified on hardware (the gloo test in
+test_sharding.py covers its host-side layout).
 """
 import ctypes as C
+import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -95,3 +101,22 @@ def test_gather_at_configs3_shard_size(comm):
         acts.free()
     finally:
         env.close()
+
+
+def test_two_rank_gather_on_two_devices(require_gpu, tmp_path):
+    """Two ranks on two devices (tests/_comm_worker.py): each steps its own shard and gathers to
+    root 0 and then all-gathers; every receiver's slots must equal each rank's own pack_rows."""
+    if _lib.load().pp3_device_count() < 2:
+        pytest.skip("needs 2 GPUs: RCCL allows one rank per device")
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_comm_worker.py")
+    env = dict(os.environ, PP3_LAUNCH_ID=f"test{os.getpid()}", PP3_RDZV_DIR=str(tmp_path))
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", str(tmp_path)], env=env) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=120) == 0
+    mine = [np.load(tmp_path / f"rows_{r}.npy") for r in range(2)]
+    nmax = mine[0].shape[0]
+    root = np.load(tmp_path / "gather_root_0.npy")
+    for r in range(2):
+        np.testing.assert_array_equal(root[r * nmax:(r + 1) * nmax], mine[r])
+        ag = np.load(tmp_path / f"allgather_{r}.npy")
+        np.testing.assert_array_equal(ag, np.concatenate(mine))

@@ -86,6 +86,50 @@ def test_tracking_camera_follows_mujoco_targetbody_rules():
         sc.camera("track", q, 240)  # the reference's default name is not in the stock model
 
 
+def _model_with_cameras(tmp_path):
+    """The stock model plus a fixed camera nested in base_link, a track camera and a targetbodycom
+    camera (advisor r02: cameras inside bodies must move with them)."""
+    import xml.etree.ElementTree as ET
+    tree = ET.parse(MODEL_XML)
+    root = tree.getroot()
+    base = next(b for b in root.iter("body") if b.get("name") == "base_link")
+    ET.SubElement(base, "camera", {"name": "nested_fixed", "pos": "0.1 0 0.05", "quat": "1 0 0 0"})
+    ET.SubElement(base, "camera", {"name": "nested_track", "mode": "track", "pos": "0 -0.5 0.3",
+                                   "xyaxes": "1 0 0 0 0.5 1"})
+    wb = root.find("worldbody")
+    ET.SubElement(wb, "camera", {"name": "com_cam", "mode": "targetbodycom", "target": "base_link",
+                                 "pos": "1 1 1"})
+    path = str(tmp_path / "cams.xml")
+    tree.write(path)
+    return render.Scene(mjcf.load(path), meshdir="/nonexistent")
+
+
+def test_nested_and_tracking_cameras_follow_mujoco_rules(tmp_path):
+    sc = _model_with_cameras(tmp_path)
+    q0 = _home_q()
+    q1 = q0.copy()
+    q1[0:3] += [0.4, -0.3, 0.1]
+    half = np.radians(30) / 2
+    q1[3:7] = [np.cos(half), 0, 0, np.sin(half)]  # base yawed 30 deg
+    R1 = mjcf.quat_to_mat(q1[3:7])
+    # fixed camera in base_link: rigidly attached (position and axes turn with the base)
+    c0, c1 = sc.camera("nested_fixed", q0, 240), sc.camera("nested_fixed", q1, 240)
+    np.testing.assert_allclose(c1[0:3], q1[0:3] + R1 @ np.array([0.1, 0, 0.05]), atol=1e-6)
+    np.testing.assert_allclose(c1[3:6], R1 @ np.array([1.0, 0, 0]), atol=1e-6)
+    np.testing.assert_allclose(c1[9:12], R1 @ np.array([0, 0, -1.0]), atol=1e-6)
+    # track: constant world offset to the body and constant world orientation (those at qpos0)
+    t0, t1 = sc.camera("nested_track", q0, 240), sc.camera("nested_track", q1, 240)
+    np.testing.assert_allclose(t1[0:3] - t0[0:3], q1[0:3] - q0[0:3], atol=1e-6)
+    np.testing.assert_allclose(t1[3:12], t0[3:12], atol=1e-7)
+    # targetbodycom: looks at base_link's subtree centre of mass (the whole robot), not its origin
+    m = sc.cm.struct
+    xpos, R, sub = sc._frames(q1)
+    c = sc.camera("com_cam", q1, 240)
+    fwd = (sub[1] - np.array([1.0, 1, 1])) / np.linalg.norm(sub[1] - np.array([1.0, 1, 1]))
+    np.testing.assert_allclose(c[9:12], fwd, atol=1e-6)
+    assert np.linalg.norm(sub[1] - xpos[1]) > 1e-3 and m.body_mass[1] > 0
+
+
 def test_cpu_restatement_draws_robot_floor_and_sky():
     sc = render.Scene(mjcf.load(MODEL_XML), meshdir="/nonexistent")
     H, W = 48, 64
