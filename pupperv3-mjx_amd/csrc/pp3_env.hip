@@ -196,24 +196,34 @@ __device__ __forceinline__ int wmax2(int v) {
 // (body_quat * joint rotation) in parallel, then lanes 0..3 compose base -> leg chain.
 // Hinge anchors coincide with body origins (jnt_pos = 0, checked at pp3_create).
 // ------------------------------------------------------------------------------------
+// The kinematics phase's per-lane model constants (lane l < 12 owns leg body bl = 2 + 3 gl + kl:
+// level kl = l / 4, leg gl = l % 4), loaded once per launch and kept in registers across the
+// substeps: otherwise every substep opens with an L2 round trip for them.
+struct KinConst {
+  float jax[3], bq[4], q0, bpos[3], cpos[3];
+};
+__device__ __forceinline__ KinConst kin_const(const DevModel& m, int l) {
+  const int lc = l < 12 ? l : 11, gl = lc & 3, kl = lc >> 2;
+  const int bl = 2 + 3 * gl + kl, jl = 1 + 3 * gl + kl, ql = 7 + 3 * gl + kl;
+  KinConst k;
+  for (int c = 0; c < 3; c++) k.jax[c] = m.jnt_axis[jl][c];
+  for (int c = 0; c < 4; c++) k.bq[c] = m.body_quat[bl][c];
+  k.q0 = m.qpos0[ql];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    k.bpos[c] = m.body_pos[bl][c];                    // this body's offset in its parent
+    k.cpos[c] = m.body_pos[kl < 2 ? bl + 1 : bl][c];  // its child's offset in it (levels 0, 1)
+  }
+  return k;
+}
+
 template <int NC>
-__device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l, bool euler) {
-  // every model constant of the phase is fetched up front (clamped lane indices, no branches)
-  // and pinned by one asm statement: one vmcnt wait instead of one per dependent use
+__device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l, bool euler, const KinConst& kc) {
   // lane l < 12 owns leg body (level kl = l / 4, leg gl = l % 4): body bl, joint jl, qpos ql
   const int lc = l < 12 ? l : 11, gl = lc & 3, kl = lc >> 2;
   const int bl = 2 + 3 * gl + kl, jl = 1 + 3 * gl + kl, ql = 7 + 3 * gl + kl;
-  float jax[3], bq[4], q0, bpos[3], cpos[3];
-  for (int c = 0; c < 3; c++) jax[c] = m.jnt_axis[jl][c];
-  for (int c = 0; c < 4; c++) bq[c] = m.body_quat[bl][c];
-  q0 = m.qpos0[ql];
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    bpos[c] = m.body_pos[bl][c];                    // this body's offset in its parent
-    cpos[c] = m.body_pos[kl < 2 ? bl + 1 : bl][c];  // its child's offset in it (levels 0, 1)
-  }
-  PIN("+v"(jax[0]), "+v"(jax[1]), "+v"(jax[2]), "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(q0),
-      "+v"(bpos[0]), "+v"(bpos[1]), "+v"(bpos[2]), "+v"(cpos[0]), "+v"(cpos[1]), "+v"(cpos[2]));
+  float jax[3] = {kc.jax[0], kc.jax[1], kc.jax[2]}, bq[4] = {kc.bq[0], kc.bq[1], kc.bq[2], kc.bq[3]}, q0 = kc.q0;
+  const float bpos[3] = {kc.bpos[0], kc.bpos[1], kc.bpos[2]}, cpos[3] = {kc.cpos[0], kc.cpos[1], kc.cpos[2]};
   // The previous substep's Euler step (eulerdamp disabled), deferred to here when `euler`: the
   // joint lanes integrate their own dof (so the new angle stays in a register), lanes 12..17 the
   // base dofs, and lane 15 integrates the base quaternion -- its axis-angle rotation shares the
@@ -1285,7 +1295,8 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
 template <int NC>
-__device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev PROF_PARAM) {
+__device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev,
+                                       const KinConst& kc PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
   l = opaque_lane(l);
   // the com and M-entry phases' lane records, loaded here without a wait: they arrive while
@@ -1307,7 +1318,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   }
   // the narrow phase's pair records for this lane's first pair, likewise (model constants)
   const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
-  kinematics(s, m, l, integrate_prev); SYNC();
+  kinematics(s, m, l, integrate_prev, kc); SYNC();
   PHASE(0); l = opaque_lane(l);
   { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
@@ -2182,6 +2193,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   LaneRec<2> re;  // plain loads (no pin): retired with the batch's first wait
   for (int k = 0; k < 2; k++)
     for (int c = 0; c < 4; c++) re.f[4 * k + c] = m.lane_env.g[k][l][c];
+  const KinConst kc = kin_const(m, l);  // (kept in registers for all substeps)
   // observation history: obs_out[36:] = obs_in[:36(H-1)] (environment.py:540-543)
   const int nmove = PP3_OBS_DIM * (m.H - 1);
   float tmp[OBS_MOVE];
@@ -2270,7 +2282,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    const int wgt = substep(s, *(const DevModel*)mp, l, h, f > 0 PROF_ARG);
+    const int wgt = substep(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
     heavy = wgt >= PP3_HEAVY2 ? 2 : (wgt >= PP3_HEAVY ? 1 : 0);
   }
   if (n_frames > 0) {  // the last substep's Euler step (the others ran inside the next kinematics)
@@ -2558,7 +2570,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   if (l < NV) { s.qvel[l] = 0.0f; s.qws[l] = 0.0f; }
   if (l < NU) s.ctrl[l] = 0.0f;
   SYNC();
-  substep(s, m, l, h, false PROF_NULL);  // pipeline_init: mjx.forward at (q, qd=0, ctrl=0)
+  substep(s, m, l, h, false, kin_const(m, l) PROF_NULL);  // pipeline_init: mjx.forward at (q, qd=0, ctrl=0)
   if (l < NQ) s.st[PP3_S_QPOS + l] = s.qpos[l];
   if (l < NV) { s.st[PP3_S_QVEL + l] = 0.0f; s.st[PP3_S_QACC_WS + l] = s.qws[l]; }
   if (l == 0) {
@@ -2613,11 +2625,12 @@ __global__ __launch_bounds__(WAVE, 2) void physics_kernel(PhysArgs a) {
   if (l < NQ) s.qpos[l] = gst[PP3_S_QPOS + l];
   if (l < NV) { s.qvel[l] = gst[PP3_S_QVEL + l]; s.qws[l] = gst[PP3_S_QACC_WS + l]; }
   if (l < NU) s.ctrl[l] = a.ctrl[(size_t)env * NU + l];
+  const KinConst kc = kin_const(m, l);
   SYNC();
   for (int i = 0; i < a.nsteps; i++) {
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    substep(s, *(const DevModel*)mp, l, h, i > 0 PROF_NULL);
+    substep(s, *(const DevModel*)mp, l, h, i > 0, kc PROF_NULL);
   }
   if (a.nsteps > 0) euler_step(s, m, l);
   if (!own) return;
