@@ -44,10 +44,11 @@ KERNEL_SOURCES = ("pupperv3-mjx_amd/csrc/pp3_env.hip", "pupperv3-mjx_amd/csrc/pp
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_current.json")
 
 
-def algorithmic_bytes_per_env_step(stride: int, H: int, dr: bool) -> int:
+def algorithmic_bytes_per_env_step(stride: int, H: int, dr: bool, trajectory: bool = False) -> int:
     """HBM bytes one env step must move (DESIGN.md 'Roofline'): state record read+write,
-    obs history read (36(H-1)) + write (36H), actions in, reward/done/metrics out, DR params."""
-    words = 2 * stride + 36 * (H - 1) + 36 * H + 12 + 2 + 19 + (62 if dr else 0)
+    obs history read (36(H-1)) + write (36H), actions in, reward/done/metrics out, DR params;
+    a fused rollout also writes the step's trajectory row (reward, done, obs 36H)."""
+    words = 2 * stride + 36 * (H - 1) + 36 * H + 12 + 2 + 19 + (62 if dr else 0) + ((2 + 36 * H) if trajectory else 0)
     return 4 * words
 
 
@@ -361,6 +362,11 @@ def main():
     ap.add_argument("--policy", type=str, default="", metavar="H1,H2,...",
                     help="policy-in-the-loop rollout: an exported-format MLP (random weights, elu) computes the "
                          "actions from the observation buffer on device before every env step")
+    ap.add_argument("--launch", choices=("rollout", "step"), default="rollout",
+                    help="rollout: the K timed steps as ONE fused launch (pp3_rollout, brax generate_unroll's "
+                         "lax.scan with the actions given up front; per-step reward/done/obs trajectories written), "
+                         "then the same K steps as K single-step launches from the same start state, timed too and "
+                         "checked bit-equal; step: K single-step launches only (pp3_step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency-floor", action="store_true",
                     help="skip the E/2-envs latency-floor launches (keeps rocprof stats to E-env launches)")
@@ -484,6 +490,18 @@ def main():
             policy.act_env(env, acts.ptr.value)
             env.step_device(acts.ptr.value)
 
+    # --launch rollout (the default for the plain env-step workloads): the timed K steps are one
+    # fused launch writing per-step trajectories; the start state is kept to replay the same K
+    # steps as single-step launches afterwards (timed, and checked bit-equal)
+    rollout = args.launch == "rollout" and policy is None and not args.gather
+    traj, snap = None, None
+    if rollout:
+        D = env.observation_size
+        traj = [_lib.DeviceBuffer(4 * args.steps * E, device), _lib.DeviceBuffer(4 * args.steps * E, device),
+                _lib.DeviceBuffer(4 * args.steps * E * D, device)]
+        snap_fields = [_abi.F_STATE, _abi.F_OBS, _abi.F_REWARD, _abi.F_DONE] + ([_abi.F_EPISODE] if args.auto_reset else [])
+        snap = {f: env._get(f) for f in snap_fields}
+
     env.synchronize()
     barrier()
     t0 = time.perf_counter()
@@ -493,6 +511,10 @@ def main():
             env.step_device(acts.ptr.value)
         env.synchronize()
         kernel_ms = (time.perf_counter() - t0) * 1e3  # policy + env step per iteration (no per-kernel events)
+    elif not args.gather and rollout:
+        _lib.check(L.pp3_rollout_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps,
+                                       traj[0].ptr, traj[1].ptr, traj[2].ptr, C.byref(ms)))
+        kernel_ms = ms.value
     elif not args.gather:
         _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps, C.byref(ms)))
         kernel_ms = ms.value
@@ -509,6 +531,35 @@ def main():
     # variants ran the same trajectories, so a timing difference is code speed, not a changed workload
     import hashlib
     state_sha16 = hashlib.sha256(env._get(_abi.F_STATE).tobytes()).hexdigest()[:16]
+    per_step = None
+    if rollout:
+        # untimed by the wall clock: the trajectories' last row against the handle's outputs, then
+        # the same K steps again as K single-step launches (HIP events) from the kept start state
+        K, D = args.steps, env.observation_size
+        last_r, last_d, last_o = np.empty(E, np.float32), np.empty(E, np.float32), np.empty(E * D, np.float32)
+        _lib.check(L.pp3_memcpy_d2h(last_r.ctypes.data_as(C.c_void_p), C.c_void_p(traj[0].ptr.value + 4 * (K - 1) * E), 4 * E))
+        _lib.check(L.pp3_memcpy_d2h(last_d.ctypes.data_as(C.c_void_p), C.c_void_p(traj[1].ptr.value + 4 * (K - 1) * E), 4 * E))
+        _lib.check(L.pp3_memcpy_d2h(last_o.ctypes.data_as(C.c_void_p), C.c_void_p(traj[2].ptr.value + 4 * (K - 1) * E * D), 4 * E * D))
+        traj_ok = (np.array_equal(last_r, env._get(_abi.F_REWARD)[:, 0]) and np.array_equal(last_d, env._get(_abi.F_DONE)[:, 0])
+                   and np.array_equal(last_o.reshape(E, D), env._get(_abi.F_OBS)))
+        end = {f: env._get(f) for f in snap}
+        for f, v in snap.items():
+            env._put(f, v)
+        env.synchronize()
+        _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, K, C.byref(ms)))
+        step_ms = ms.value
+        # bitwise (the state record holds the rng key words as float bit patterns, some of them NaNs)
+        differ = [int(f) for f, v in end.items() if not np.array_equal(env._get(f).view(np.uint32), v.view(np.uint32))]
+        same = not differ
+        per_step = {"launches": K, "avg_launch_ms": round(step_ms / K, 4),
+                    "kernel_env_steps_per_s": round(E * K / (step_ms / 1e3), 1),
+                    "bit_equal_to_rollout": bool(same), "trajectory_last_row_equals_outputs": bool(traj_ok)}
+        if differ:
+            per_step["differing_fields"] = differ
+        if not (same and traj_ok):
+            print(f"rank {rank}: fused rollout differs from single-step launches: {per_step}", file=sys.stderr, flush=True)
+        for b in traj:
+            b.free()
     gather_info = None
     if args.gather:
         # untimed: the same K steps' kernels alone (events), then the gather alone
@@ -547,19 +598,26 @@ def main():
     if rank == 0:
         K = args.steps
         value = E * world * K / wall_max
-        launch_s = kernel_ms_max / 1e3 / K
-        bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr)
+        launch_s = kernel_ms_max / 1e3 / K  # kernel time per env step of the batch
+        spl = K if rollout else 1  # env steps per launch
+        bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr,
+                                             trajectory=rollout)
         achieved = bpe * E / launch_s / 1e9
         traffic, valu, epw, tsrc, flops, fsrc = None, None, 2, None, None, None
         if os.path.exists(TRAFFIC_FILE):
+            # PMC figures of this kernel build and launch shape, per env step of the batch
+            # (profiles/traffic_current.json: per-launch values over steps_per_launch)
             tj = json.load(open(TRAFFIC_FILE))
             if (tj.get("src_sha16") == kernel_source_sha16() and tj.get("envs") == E
-                    and tj.get("dr", False) == args.dr and not args.obstacles):
-                traffic = tj.get("hbm_bytes_per_launch")
-                valu = tj.get("valu_insts_per_wave")
+                    and tj.get("dr", False) == args.dr and not args.obstacles
+                    and tj.get("launch", "step") == ("rollout" if rollout else "step")):
+                tspl = tj.get("steps_per_launch", 1)
+                traffic = tj.get("hbm_bytes_per_launch") / tspl * spl
+                valu = tj.get("valu_insts_per_wave") / tspl
                 epw = tj.get("envs_per_wave", 2)
                 tsrc = tj.get("source")
-                flops, fsrc = tj.get("fp32_flops_per_launch"), tj.get("fp32_flops_source")
+                if tj.get("fp32_flops_per_launch"):
+                    flops, fsrc = tj.get("fp32_flops_per_launch") / tspl, tj.get("fp32_flops_source")
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -586,9 +644,16 @@ def main():
                        "commands": "reset-sampled, resampled every 500 steps" if args.random_commands else "fixed (0.5,0,0)",
                        "gather": gather_info, "gather_check": gcheck, "comm": comm_kind, "auto_reset_episode_length": args.auto_reset or None,
                        "policy_in_loop": args.policy or None},
+            "launch": (f"rollout: the {K} timed steps fused into one pp3_rollout launch (per-step reward/done/obs "
+                       "trajectories written); per_step_launch = the same steps as single-step launches"
+                       if rollout else "step: one pp3_step launch per env step"),
+            "per_step_launch": per_step,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "kernel": "pp3::env_step_kernel", "bytes_per_env_step": bpe,
+                         "kernel": "pp3::env_step_kernel<%d, %s>" % (env.config_struct.ncon_max or 8, "true" if rollout else "false"),
+                         "steps_per_launch": spl, "bytes_per_env_step": bpe,
+                         "algorithmic_bytes_per_launch": bpe * E * spl,
+                         "launch_ms": round(launch_s * spl * 1e3, 4),
                          "avg_launch_ms": round(launch_s * 1e3, 4),
                          "traffic_source": tsrc or "none for this kernel build (profiles/traffic_current.json "
                                                    "src_sha16 != the kernel sources' hash)"},
@@ -624,7 +689,10 @@ def main():
             half._put(_abi.F_STATE, hrec)
             _lib.check(L.pp3_step_timed(half._h, acts.ptr, E // 2 * 12, args.warmup or 5, C.byref(ms)))
             hk = min(args.steps, 100)
-            _lib.check(L.pp3_step_timed(half._h, acts.ptr, E // 2 * 12, hk, C.byref(ms)))
+            if rollout:  # the same launch shape as the measured one
+                _lib.check(L.pp3_rollout_timed(half._h, acts.ptr, E // 2 * 12, hk, None, None, None, C.byref(ms)))
+            else:
+                _lib.check(L.pp3_step_timed(half._h, acts.ptr, E // 2 * 12, hk, C.byref(ms)))
             half_s = ms.value / 1e3 / hk
             half.close()
             out["roofline"]["latency"] = {"envs": E // 2, "waves_per_simd": (E // 2) / 2 / N_SIMD,

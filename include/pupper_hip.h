@@ -342,6 +342,18 @@ int32_t pp3_env_device(const pp3_env_t* env);
 int pp3_reset(pp3_env_t* env, const uint32_t* keys_dev, const uint8_t* mask_dev, void* stream);
 /* step(state, action): actions_dev = f32[N][12].  environment.py:348-483. */
 int pp3_step(pp3_env_t* env, const float* actions_dev, void* stream);
+/* nsteps env steps fused into one launch: the unroll of brax's PPO generate_unroll (a lax.scan of
+ * env.step, [ext] brax 0.12.1 training/acting.py) with the actions given up front.  Step t reads
+ * actions_dev + t * action_stride (elements; 0 = the same action every step) and is the same
+ * computation as the t-th of nsteps pp3_step calls (bit for bit); the handle ends in the same
+ * state.  Optional trajectory outputs (device, NULL = not written): reward_dev f32[nsteps][N],
+ * done_dev f32[nsteps][N], obs_dev f32[nsteps][N][36H] -- step t's reward, done and observation
+ * as pp3_step leaves them in the handle (auto-reset: the reset's obs for done envs).  Each wave
+ * runs its two envs' steps back to back, so the launch ends with the slowest wave's SUM of step
+ * times instead of every step waiting for that step's slowest wave.  With auto-reset and
+ * action_repeat > 1 every wrapper step stays `repeat` launches. */
+int pp3_rollout(pp3_env_t* env, const float* actions_dev, int64_t action_stride, int32_t nsteps, float* reward_dev,
+                float* done_dev, float* obs_dev, void* stream);
 /* Per-env DR parameters f32[N][62] (device), or NULL to disable DR. */
 int pp3_set_dr(pp3_env_t* env, const float* dr_dev);
 int pp3_set_pipeline_output(pp3_env_t* env, int32_t enable);
@@ -422,6 +434,9 @@ int pp3_fill_uniform(pp3_env_t* env, float* dev, int64_t count, uint32_t seed, u
  * kernel_ms_total receives their elapsed time. */
 int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stride, int32_t nsteps,
                    float* kernel_ms_total);
+/* The same for one pp3_rollout over nsteps (trajectory outputs as pp3_rollout). */
+int pp3_rollout_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stride, int32_t nsteps,
+                      float* reward_dev, float* done_dev, float* obs_dev, float* kernel_ms_total);
 
 /* Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-clock totals of env_step_kernel
  * summed over envs (n <= 16 slots); returns PP3_ERR_ARG in the production build. */

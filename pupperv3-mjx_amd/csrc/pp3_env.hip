@@ -2133,6 +2133,8 @@ __device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m,
 // kernels: workgroup b = one wave = envs 2b (lanes 0..31) and 2b+1 (lanes 32..63).  With an
 // odd N the last wave's second half recomputes env N-1 and stores nothing.
 // ------------------------------------------------------------------------------------
+struct StepArgs;
+typedef __attribute__((address_space(4))) const StepArgs GArgs;
 struct StepArgs {
   const DevModel* m;
   float* state;          // [N][stride]
@@ -2150,32 +2152,51 @@ struct StepArgs {
   int episode_length;
   int repeat, phase;  // auto-reset mode: action_repeat and this launch's repeat index
   int N;
+  int nsteps;            // env steps per launch (a fused rollout: step t reads actions + t * act_stride)
+  int64_t act_stride;
+  float* traj_reward;    // fused rollout outputs, each optional: [nsteps][N]
+  float* traj_done;      // [nsteps][N]
+  float* traj_obs;       // [nsteps][N][36H]
 };
 
-template <int NC>
-__global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
+template <int NC, bool FUSED>
+__global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   __shared__ Shared<NC> sh[2];
-  const int lane = threadIdx.x;
-  const int h = lane >> 5, l = lane & (HW - 1);
-  const int env_raw = 2 * blockIdx.x + h;
-  const bool own = env_raw < a.N;
-  const int env = own ? env_raw : a.N - 1;
-  Shared<NC>& s = sh[h];
-  const DevModel& m = *(const DevModel*)(const GModel*)a.m;  // constant AS: uniform reads -> s_load
-  const int stride = m.stride;
-  const int part = m.partitionable;
-  float* gst = a.state + (size_t)env * stride;
+  const int nsteps = FUSED ? a_arg.nsteps : 1;
 #ifdef PP3_PHASE_PROF
   const uint32_t t_start_ = shader_cycles();
   const uint32_t rt_start_ = (uint32_t)__builtin_amdgcn_s_memrealtime();  // 100 MHz, chip-wide
   Prof pf_local{t_start_, 0u, t_start_, 0u, 0u, 0u, 0u, 0u, 0u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   Prof* pf = &pf_local;
 #endif
+  // FUSED (pp3_rollout): the wave runs its two envs' nsteps steps back to back, each step reading
+  // back the previous one's global stores (state record, lag rows, obs history; the fence at the
+  // bottom).  The arguments are re-read every step through an opaque kernarg pointer and the lane
+  // id is opaque too: otherwise the argument / model loads and the lane masks are hoisted out of
+  // the loop and kept live across it (SGPR and VGPR spills).  With FUSED false the loop runs once
+  // and the kernel compiles to the single-step code it always was.
+  for (int it = 0;;) {
+  const GArgs* ap = (const GArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  if (FUSED) asm volatile("" : "+s"(ap));
+  const StepArgs& a = FUSED ? *(const StepArgs*)ap : a_arg;
+  int lane = threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)
+  if (FUSED) asm volatile("" : "+v"(lane));
+  const int h = lane >> 5, l = lane & (HW - 1);
+  Shared<NC>& s = sh[h];
+  const int env_raw = 2 * blockIdx.x + h;
+  const bool own = env_raw < a.N;
+  const int env = own ? env_raw : a.N - 1;
+  const DevModel& m = *(const DevModel*)(const GModel*)a.m;  // constant AS: uniform reads -> s_load
+  const int stride = m.stride;
+  const int part = m.partitionable;
+  float* gst = a.state + (size_t)env * stride;
+  // fused rollout: this step's observation row of the trajectory (optional)
+  float* const to = FUSED && a.traj_obs ? a.traj_obs + ((size_t)it * a.N + env) * (PP3_OBS_DIM * m.H) : nullptr;
   // ---- every global load of this env step issued together (one memory round trip): state
   // record head, this lane's action-latency row and IMU row, the action, the obs history, the
   // lane's env constants and body parameters; the global stores only after all of them ----
   int n_frames = __builtin_amdgcn_readfirstlane(m.n_frames);
-  const float* act_env = a.actions + (size_t)env * NU;
+  const float* act_env = a.actions + (size_t)it * a.act_stride + (size_t)env * NU;
   const size_t obs_base = (size_t)env * (PP3_OBS_DIM * m.H);
   const float* oi = a.obs_in + obs_base;
   float* oo = a.obs_out + obs_base;
@@ -2217,7 +2238,10 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (own)
 #pragma unroll
     for (int t = 0; t < OBS_MOVE; t++)
-      if (l + HW * t < nmove) oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
+      if (l + HW * t < nmove) {
+        oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
+        if (FUSED && to) to[PP3_OBS_DIM + l + HW * t] = tmp[t];
+      }
 #pragma unroll
   for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
     if (l + HW * t < PP3_S_ACT_BUF) s.st[l + HW * t] = v[t];
@@ -2307,7 +2331,10 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   get_obs(s, m, gst + m.imu_off, l, h, re.f[LE_POSE16], own, imu_stash PROF_ARG);
   {
     if (own)
-      for (int k = l; k < PP3_OBS_DIM; k += HW) oo[k] = s.x.e.o[k];
+      for (int k = l; k < PP3_OBS_DIM; k += HW) {
+        oo[k] = s.x.e.o[k];
+        if (FUSED && to) to[k] = s.x.e.o[k];
+      }
   }
   SYNC();
   if (l < NQ) s.st[PP3_S_QPOS + l] = s.qpos[l];
@@ -2454,6 +2481,10 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
   if (own && l == 0) {
     a.reward[env] = rout;
     if (!a.episode || last) a.done[env] = done_out ? 1.0f : 0.0f;
+    if (FUSED && (!a.episode || last)) {
+      if (a.traj_reward) a.traj_reward[(size_t)it * a.N + env] = rout;
+      if (a.traj_done) a.traj_done[(size_t)it * a.N + env] = done_out ? 1.0f : 0.0f;
+    }
     a.metrics[(size_t)env * PP3_NMETRIC] =
         sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
   }
@@ -2479,7 +2510,10 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
     const float* fo = a.first_obs + (size_t)env * PP3_OBS_DIM * m.H;
     __threadfence_block();  // the prologue's history stores (other lanes, same addresses) land first
     if (own)
-      for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) oo[i] = fo[i];
+      for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) {
+        oo[i] = fo[i];
+        if (FUSED && to) to[i] = fo[i];
+      }
   }
   SYNC();
   if (own)
@@ -2488,7 +2522,13 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a) {
       if (l + HW * t < PP3_S_ACT_BUF) gst[l + HW * t] = s.st[l + HW * t];
   PHASE(12);
   }
+  if (!FUSED || ++it >= nsteps) break;
+  // the next step reads back this step's global stores (state record, lag rows, obs history)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
 #ifdef PP3_PHASE_PROF
+  const int lane = threadIdx.x;
   if (lane < NPROF - 1 && blockIdx.x < MAXWAVE) g_prof[blockIdx.x][lane] += pf->acc;
   if (lane == 0 && blockIdx.x < MAXWAVE) {
     uint32_t hwid, xcc;
@@ -3257,8 +3297,12 @@ int pp3_reset(pp3_env_t* e, const uint32_t* keys_dev, const uint8_t* mask_dev, v
   return PP3_OK;
 }
 
-int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
-  if (!e || !actions_dev) return set_err(PP3_ERR_ARG, "pp3_step: null argument");
+// One env step per launch (pp3_step), or nsteps fused into each launch (pp3_rollout: every wave
+// runs its envs' steps back to back, so a slow wave of step t no longer holds up the whole batch
+// at step t + 1).  With action_repeat > 1 (auto-reset mode) each wrapper step stays `repeat`
+// single-step launches.
+static int launch_steps(pp3_env_t* e, const float* actions_dev, int64_t action_stride, int32_t nsteps,
+                        float* traj_reward, float* traj_done, float* traj_obs, bool fused, void* stream) {
   HIPCHK(hipSetDevice(e->device));
   StepArgs a;
   a.m = e->dmodel;
@@ -3277,12 +3321,42 @@ int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
   a.episode_length = e->episode_length;
   a.N = e->N;
   a.repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;
-  for (a.phase = 0; a.phase < a.repeat; a.phase++) {  // action_repeat: the same action, k launches
-    if (e->nc == 8) hipLaunchKernelGGL(env_step_kernel<8>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
-    else hipLaunchKernelGGL(env_step_kernel<16>, dim3((e->N + 1) / 2), dim3(WAVE), 0, stream_of(e, stream), a);
-    HIPCHK(hipGetLastError());
+  a.act_stride = action_stride;
+  const bool one_launch = fused && a.repeat == 1;
+  a.nsteps = one_launch ? nsteps : 1;
+  const dim3 grid((e->N + 1) / 2), block(WAVE);
+  const hipStream_t st = stream_of(e, stream);
+  const size_t on = (size_t)e->N * PP3_OBS_DIM * e->H;
+  for (int t = 0; t < (one_launch ? 1 : nsteps); t++) {
+    a.actions = actions_dev + (one_launch ? 0 : (size_t)t * (size_t)action_stride);
+    a.traj_reward = traj_reward ? traj_reward + (one_launch ? 0 : (size_t)t * e->N) : nullptr;
+    a.traj_done = traj_done ? traj_done + (one_launch ? 0 : (size_t)t * e->N) : nullptr;
+    a.traj_obs = traj_obs ? traj_obs + (one_launch ? 0 : (size_t)t * on) : nullptr;
+    for (a.phase = 0; a.phase < a.repeat; a.phase++) {  // action_repeat: the same action, k launches
+      if (fused) {
+        if (e->nc == 8) hipLaunchKernelGGL((env_step_kernel<8, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((env_step_kernel<16, true>), grid, block, 0, st, a);
+      } else {
+        if (e->nc == 8) hipLaunchKernelGGL((env_step_kernel<8, false>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((env_step_kernel<16, false>), grid, block, 0, st, a);
+      }
+      HIPCHK(hipGetLastError());
+    }
   }
   return PP3_OK;
+}
+
+int pp3_step(pp3_env_t* e, const float* actions_dev, void* stream) {
+  if (!e || !actions_dev) return set_err(PP3_ERR_ARG, "pp3_step: null argument");
+  return launch_steps(e, actions_dev, 0, 1, nullptr, nullptr, nullptr, false, stream);
+}
+
+int pp3_rollout(pp3_env_t* e, const float* actions_dev, int64_t action_stride, int32_t nsteps, float* reward_dev,
+                float* done_dev, float* obs_dev, void* stream) {
+  if (!e || !actions_dev) return set_err(PP3_ERR_ARG, "pp3_rollout: null argument");
+  if (nsteps < 1) return set_err(PP3_ERR_ARG, "pp3_rollout: nsteps must be >= 1");
+  if (action_stride < 0) return set_err(PP3_ERR_ARG, "pp3_rollout: negative action_stride");
+  return launch_steps(e, actions_dev, action_stride, nsteps, reward_dev, done_dev, obs_dev, true, stream);
 }
 
 void* pp3_stream(pp3_env_t* e) { return e ? (void*)e->stream : nullptr; }
@@ -3562,6 +3636,19 @@ int pp3_step_timed(pp3_env_t* e, const float* actions_dev, int64_t action_stride
     int rc = pp3_step(e, actions_dev + (size_t)i * (size_t)action_stride, e->stream);
     if (rc) return rc;
   }
+  HIPCHK(hipEventRecord(e->ev1, e->stream));
+  HIPCHK(hipEventSynchronize(e->ev1));
+  HIPCHK(hipEventElapsedTime(kernel_ms_total, e->ev0, e->ev1));
+  return PP3_OK;
+}
+
+int pp3_rollout_timed(pp3_env_t* e, const float* actions_dev, int64_t action_stride, int32_t nsteps,
+                      float* reward_dev, float* done_dev, float* obs_dev, float* kernel_ms_total) {
+  if (!e || !actions_dev || !kernel_ms_total) return set_err(PP3_ERR_ARG, "null argument");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipEventRecord(e->ev0, e->stream));
+  const int rc = pp3_rollout(e, actions_dev, action_stride, nsteps, reward_dev, done_dev, obs_dev, e->stream);
+  if (rc) return rc;
   HIPCHK(hipEventRecord(e->ev1, e->stream));
   HIPCHK(hipEventSynchronize(e->ev1));
   HIPCHK(hipEventElapsedTime(kernel_ms_total, e->ev0, e->ev1));

@@ -44,6 +44,7 @@ def load() -> C.CDLL:
     L.pp3_env_device.restype = i32
     L.pp3_reset.argtypes = [vp, vp, vp, vp]
     L.pp3_step.argtypes = [vp, vp, vp]
+    L.pp3_rollout.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
     L.pp3_set_dr.argtypes = [vp, vp]
     L.pp3_set_pipeline_output.argtypes = [vp, i32]
     L.pp3_physics_step.argtypes = [vp, vp, i32, vp]
@@ -62,6 +63,7 @@ def load() -> C.CDLL:
     L.pp3_memcpy_d2d.argtypes = [vp, vp, sz, vp]
     L.pp3_fill_uniform.argtypes = [vp, vp, i64, C.c_uint32, C.c_uint32, C.c_float, C.c_float, vp]
     L.pp3_step_timed.argtypes = [vp, vp, i64, i32, C.POINTER(C.c_float)]
+    L.pp3_rollout_timed.argtypes = [vp, vp, i64, i32, vp, vp, vp, C.POINTER(C.c_float)]
     L.pp3_phase_profile.argtypes = [C.POINTER(C.c_uint64), i32, i32]
     L.pp3_wave_profile.argtypes = [C.POINTER(C.c_uint32), i32]
     L.pp3_set_auto_reset.argtypes = [vp, i32]
@@ -90,7 +92,7 @@ def load() -> C.CDLL:
     L.pp3_render_last_error.restype = C.c_char_p
     L.pp3_comm_allreduce.argtypes = [vp, vp, vp, i32, i32]
     L.pp3_comm_barrier.argtypes = [vp]
-    for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_set_dr", "pp3_set_pipeline_output",
+    for name in ("pp3_create", "pp3_destroy", "pp3_reset", "pp3_step", "pp3_rollout", "pp3_rollout_timed", "pp3_set_dr", "pp3_set_pipeline_output",
                  "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host",
                  "pp3_synchronize", "pp3_copy_field_to_host_async", "pp3_host_malloc", "pp3_host_free",
                  "pp3_memcpy_h2d_async",
@@ -122,11 +124,11 @@ def check_comm(rc: int) -> None:
 
 EXPORTED_SYMBOLS = (
     "pp3_abi_version", "pp3_struct_size", "pp3_last_error", "pp3_device_count", "pp3_create", "pp3_destroy",
-    "pp3_num_envs", "pp3_state_stride", "pp3_env_device", "pp3_reset", "pp3_step", "pp3_set_dr",
+    "pp3_num_envs", "pp3_state_stride", "pp3_env_device", "pp3_reset", "pp3_step", "pp3_rollout", "pp3_set_dr",
     "pp3_set_pipeline_output", "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
     "pp3_copy_field_to_host_async", "pp3_host_malloc", "pp3_host_free", "pp3_memcpy_h2d_async",
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
-    "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
+    "pp3_fill_uniform", "pp3_step_timed", "pp3_rollout_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
     "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
     "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_comm_rank", "pp3_comm_world",

@@ -522,6 +522,51 @@ class PupperV3Env:
         self.step_device(self._act_buf.ptr.value)
         return self._issue(single)
 
+    def rollout_device(self, actions_dev: int, action_stride: int, nsteps: int, reward_dev: Optional[int] = None,
+                       done_dev: Optional[int] = None, obs_dev: Optional[int] = None,
+                       stream: Optional[int] = None) -> None:
+        """pp3_rollout: `nsteps` steps fused into one launch; step t reads actions_dev + t *
+        action_stride floats; optional trajectory outputs reward/done f32[nsteps][N], obs
+        f32[nsteps][N][36H] (device pointers)."""
+        self._before_launch()
+        vp = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        _lib.check(self._L.pp3_rollout(self._h, C.c_void_p(actions_dev), int(action_stride), int(nsteps),
+                                       vp(reward_dev), vp(done_dev), vp(obs_dev), vp(stream)))
+
+    def rollout(self, state: State, actions) -> Tuple[State, Dict[str, np.ndarray]]:
+        """The unroll of brax's generate_unroll ([ext] brax 0.12.1 training/acting.py: a lax.scan of
+        env.step) with the K actions given up front, as ONE fused launch: returns the state after
+        the last step (what K step() calls return) and the per-step trajectory {"obs": [K, N, 36H],
+        "reward": [K, N], "done": [K, N]} (single-env states: [K, 36H] / [K]).  Bit for bit the
+        same as K step() calls."""
+        single = np.ndim(state.reward) == 0
+        n, D = self.num_envs, self.observation_size
+        act = np.ascontiguousarray(np.asarray(actions, dtype=np.float32))
+        if act.ndim < 2 or act.size % (n * _abi.NU):
+            raise ValueError(f"actions must be [K, {n}, {_abi.NU}] (got {np.shape(actions)})")
+        K = act.size // (n * _abi.NU)
+        if not self.holds(state):
+            self._write_state(state)
+        bufs = [_lib.DeviceBuffer(act.nbytes, self.device), _lib.DeviceBuffer(4 * K * n, self.device),
+                _lib.DeviceBuffer(4 * K * n, self.device), _lib.DeviceBuffer(4 * K * n * D, self.device)]
+        try:
+            bufs[0].upload(act)
+            self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, bufs[1].ptr.value, bufs[2].ptr.value,
+                                bufs[3].ptr.value)
+            self.synchronize()
+            rew = np.empty((K, n), np.float32)
+            done = np.empty((K, n), np.float32)
+            obs = np.empty((K, n, D), np.float32)
+            for b, a in zip(bufs[1:], (rew, done, obs)):
+                b.download(a)
+        finally:
+            for b in bufs:
+                b.free()
+        traj = {"obs": obs, "reward": rew, "done": done}
+        if single:
+            traj = {k: v[:, 0] for k, v in traj.items()}
+        return self._issue(single), traj
+
     def holds(self, state: State) -> bool:
         """The device buffers hold exactly `state`: the last state this env issued, unedited, and
         no launch or upload since."""

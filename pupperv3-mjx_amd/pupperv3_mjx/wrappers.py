@@ -89,6 +89,16 @@ class AutoResetEpisodeEnv:
         return st
 
     def step(self, state: State, action) -> State:
+        self._prepare(state)
+        return self.env.step(state, action)
+
+    def rollout(self, state: State, actions):
+        """K wrapper steps as one fused launch (PupperV3Env.rollout; action_repeat > 1 keeps its
+        k launches per step): (state after the last step, {"obs", "reward", "done"} per step)."""
+        self._prepare(state)
+        return self.env.rollout(state, actions)
+
+    def _prepare(self, state: State) -> None:
         n = self.env.num_envs
         if not self.env.holds(state):
             # an edited (or foreign) state: its episode record and done go back with it (env.step
@@ -102,7 +112,6 @@ class AutoResetEpisodeEnv:
                 ep[:, _abi.EP_LENGTH] = np.asarray(info["episode_metrics"]["length"], dtype=np.float32).reshape(n)
                 self.env._put(_abi.F_EPISODE, ep)
             self.env._put(_abi.F_DONE, np.asarray(state.done, dtype=np.float32).reshape(n, 1))
-        return self.env.step(state, action)
 
 
 def wrap(env: PupperV3Env, episode_length: int = 1000, action_repeat: int = 1,

@@ -13,4 +13,4 @@ rc=$?; echo "tests_rc=$rc"; tail -n 4 $OUT/gpu_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
 timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $OUT/bench_driver.json 2> $OUT/bench_driver.err || { tail $OUT/bench_driver.err; exit 1; }
-python3 -c "import json; d=json.loads(open('$OUT/bench_driver.json').read().strip().split('\n')[-1]); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['state_sha16'], d['n_gpus'])"
+python3 -c "import json; d=json.loads(open('$OUT/bench_driver.json').read().strip().split('\n')[-1]); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d.get('per_step_launch') and d['per_step_launch']['avg_launch_ms'], d['state_sha16'], d['n_gpus'])"

@@ -14,7 +14,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from summarize_profile import _pmc  # noqa: E402
+from summarize_profile import _arg, _kernel, _pmc  # noqa: E402
 
 ENVS = 4096
 
@@ -23,11 +23,12 @@ def main():
     d = sys.argv[1]
     c = _pmc(os.path.join(d, "pmc_flops"))
     if not c:
-        raise SystemExit(f"no env_step_kernel counters under {d}/pmc_flops")
+        raise SystemExit(f"no {_kernel()} counters under {d}/pmc_flops")
+    spl = int(_arg("--steps-per-launch", 50 if _arg("--launch", "rollout") == "rollout" else 1))
     fma, add, mul, trans = (c.get("SQ_INSTS_VALU_%s_F32" % k, 0.0) for k in ("FMA", "ADD", "MUL", "TRANS"))
     flops = 64.0 * (2 * fma + add + mul + trans)
-    out = {"counters_per_launch": c, "fp32_flops_per_launch": flops, "envs": ENVS,
-           "fp32_flops_per_env_step": flops / ENVS,
+    out = {"kernel": _kernel(), "steps_per_launch": spl, "counters_per_launch": c, "fp32_flops_per_launch": flops,
+           "envs": ENVS, "fp32_flops_per_env_step": flops / ENVS / spl,
            "fp32_share_of_valu": (fma + add + mul + trans) / max(c.get("SQ_INSTS_VALU", 1.0), 1.0)}
     print(json.dumps(out, indent=1))
     if "--commit" in sys.argv:
@@ -38,7 +39,7 @@ def main():
         import bench
         tf = os.path.join(root, "profiles", "traffic_current.json")
         tj = json.load(open(tf))
-        if tj.get("src_sha16") != bench.kernel_source_sha16():
+        if tj.get("src_sha16") != bench.kernel_source_sha16() or tj.get("steps_per_launch", 1) != spl:
             raise SystemExit("traffic_current.json is for another kernel build: re-run tools/gpu_profile.sh first")
         tj["fp32_flops_per_launch"] = flops
         tj["fp32_flops_source"] = dst + "_flops_pmc.json (tools/gpu_flops.sh on MI355X)"

@@ -1,6 +1,11 @@
 """Summarise a tools/gpu_profile.sh output directory (kernel stats + PMC passes) for env_step_kernel.
 
-  python tools/summarize_profile.py gpurun_out/<tag> [--commit profiles/r01_vN]
+  python tools/summarize_profile.py gpurun_out/<tag> [--commit profiles/r01_vN] [--launch step]
+
+The bench's default launch is a fused rollout (pp3_rollout, `env_step_kernel<8, true>`, one
+dispatch of --steps env steps); its single-step replay and the warmup are `env_step_kernel<8,
+false>` dispatches, kept apart here.  --launch step summarises the single-step kernel instead
+(a `bench.py --launch step` profile).  Per-launch figures are also given per env step.
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KB; per MI355X_MICROARCH.md (HBM /
 rocprofv3 section) FETCH_SIZE on gfx950 reports half the bytes of wide coalesced reads, so it is
@@ -15,7 +20,15 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNEL = "env_step_kernel"
+KERNEL = "env_step_kernel<8, true>"
+
+
+def _arg(name, default):
+    return sys.argv[sys.argv.index(name) + 1] if name in sys.argv else default
+
+
+def _kernel():
+    return "env_step_kernel<8, false>" if _arg("--launch", "rollout") == "step" else KERNEL
 
 
 def _pmc(d):
@@ -23,18 +36,20 @@ def _pmc(d):
     agg = defaultdict(list)
     for f in files:
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"]:
+            if _kernel() in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
 def main():
     d = sys.argv[1]
-    out = {}
+    launch = _arg("--launch", "rollout")
+    spl = int(_arg("--steps-per-launch", 50 if launch == "rollout" else 1))  # gpu_profile.sh: --steps 50
+    out = {"kernel": _kernel(), "launch": launch, "steps_per_launch": spl}
     stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         for r in csv.DictReader(open(stats[0])):
-            if KERNEL in r["Name"]:
+            if _kernel() in r["Name"]:
                 out["kernel_avg_ns"] = float(r["AverageNs"])
                 out["kernel_calls"] = int(r["Calls"])
     sq = _pmc(os.path.join(d, "pmc_sq"))
@@ -48,6 +63,9 @@ def main():
         out["fetch_bytes_per_launch"] = 2 * f * 1024   # gfx950 FETCH_SIZE x2 correction
         out["write_bytes_per_launch"] = w * 1024
         out["hbm_bytes_per_launch"] = out["fetch_bytes_per_launch"] + out["write_bytes_per_launch"]
+        out["hbm_bytes_per_env_step"] = out["hbm_bytes_per_launch"] / spl / 4096
+    if "per_wave" in out:
+        out["per_wave_per_step"] = {k: v / spl for k, v in out["per_wave"].items()}
     print(json.dumps(out, indent=1))
     if "--commit" in sys.argv:
         dst = sys.argv[sys.argv.index("--commit") + 1]
@@ -62,6 +80,7 @@ def main():
             json.dump({"source": dst + "_pmc_summary.json (tools/gpu_profile.sh on MI355X, bench.py --steps 50 --warmup 5 "
                                      "--no-latency-floor --no-extras)",
                        "src_sha16": bench.kernel_source_sha16(), "envs": 4096, "dr": False,
+                       "kernel": out["kernel"], "launch": launch, "steps_per_launch": spl,
                        "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
                        "fetch_bytes_per_launch": out["fetch_bytes_per_launch"],
                        "write_bytes_per_launch": out["write_bytes_per_launch"],
