@@ -2175,6 +2175,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   // id is opaque too: otherwise the argument / model loads and the lane masks are hoisted out of
   // the loop and kept live across it (SGPR and VGPR spills).  With FUSED false the loop runs once
   // and the kernel compiles to the single-step code it always was.
+  int heavy_prev = 0;  // fused: the load flag carries over into the next step's first substep
   for (int it = 0;;) {
   const GArgs* ap = (const GArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   if (FUSED) asm volatile("" : "+s"(ap));
@@ -2292,7 +2293,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   uint32_t hwid;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
   const int wslot = (int)(hwid & 1u);
-  int heavy = 0;  // the previous substep's load was high (1) / very high (2): this wave sets the launch's tail
+  int heavy = heavy_prev;  // the previous substep's load was high (1) / very high (2): this wave sets the launch's tail
   for (int f = 0; f < n_frames; f++) {
     // the heavy waves (many contacts, leg-leg Newton path) ahead of their partners, which have
     // slack; between equals the two slots alternate
@@ -2522,6 +2523,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
       if (l + HW * t < PP3_S_ACT_BUF) gst[l + HW * t] = s.st[l + HW * t];
   PHASE(12);
   }
+  heavy_prev = heavy;
   if (!FUSED || ++it >= nsteps) break;
   // the next step reads back this step's global stores (state record, lag rows, obs history)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
