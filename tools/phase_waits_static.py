@@ -20,7 +20,7 @@ def main():
     if len(sys.argv) == 1:
         subprocess.run(["make", "-s", "-C", CSRC, "asm-prof"], check=True, stderr=subprocess.DEVNULL)
     s = open(path).read()
-    a = s.index("_ZN3pp315env_step_kernelILi8EEEvNS_8StepArgsE:")
+    a = s.index("_ZN3pp315env_step_kernelILi8ELb1EEEvNS_8StepArgsE:")
     body = s[a:s.index(".Lfunc_end", a)].split("\n")
     seg = Counter()
     tot = Counter()
