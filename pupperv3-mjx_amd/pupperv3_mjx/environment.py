@@ -429,6 +429,9 @@ class PupperV3Env:
         if getattr(self, "_h", None):
             self._L.pp3_destroy(self._h)
             self._h = None
+        for b in (getattr(self, "_roll_bufs", None) or (0, []))[1]:
+            b.free()
+        self._roll_bufs = None
 
     def __del__(self):
         try:
@@ -547,25 +550,33 @@ class PupperV3Env:
         K = act.size // (n * _abi.NU)
         if not self.holds(state):
             self._write_state(state)
-        bufs = [_lib.DeviceBuffer(act.nbytes, self.device), _lib.DeviceBuffer(4 * K * n, self.device),
-                _lib.DeviceBuffer(4 * K * n, self.device), _lib.DeviceBuffer(4 * K * n * D, self.device)]
-        try:
-            bufs[0].upload(act)
-            self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, bufs[1].ptr.value, bufs[2].ptr.value,
-                                bufs[3].ptr.value)
-            self.synchronize()
-            rew = np.empty((K, n), np.float32)
-            done = np.empty((K, n), np.float32)
-            obs = np.empty((K, n, D), np.float32)
-            for b, a in zip(bufs[1:], (rew, done, obs)):
-                b.download(a)
-        finally:
-            for b in bufs:
-                b.free()
+        bufs = self._rollout_buffers(K)
+        bufs[0].upload(act)
+        self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, bufs[1].ptr.value, bufs[2].ptr.value,
+                            bufs[3].ptr.value)
+        self.synchronize()
+        rew = np.empty((K, n), np.float32)
+        done = np.empty((K, n), np.float32)
+        obs = np.empty((K, n, D), np.float32)
+        for b, a in zip(bufs[1:], (rew, done, obs)):
+            b.download(a)
         traj = {"obs": obs, "reward": rew, "done": done}
         if single:
             traj = {k: v[:, 0] for k, v in traj.items()}
         return self._issue(single), traj
+
+    def _rollout_buffers(self, K: int) -> list:
+        """Device buffers of rollout(): actions, reward, done, obs for K steps (kept and grown)."""
+        cur = getattr(self, "_roll_bufs", None)
+        if cur is None or cur[0] < K:
+            if cur is not None:
+                for b in cur[1]:
+                    b.free()
+            n, D = self.num_envs, self.observation_size
+            cur = (K, [_lib.DeviceBuffer(4 * K * n * _abi.NU, self.device), _lib.DeviceBuffer(4 * K * n, self.device),
+                       _lib.DeviceBuffer(4 * K * n, self.device), _lib.DeviceBuffer(4 * K * n * D, self.device)])
+            self._roll_bufs = cur
+        return cur[1]
 
     def holds(self, state: State) -> bool:
         """The device buffers hold exactly `state`: the last state this env issued, unedited, and

@@ -52,3 +52,13 @@ def test_create_rejects_bad_config_without_gpu_work():
 def test_state_layout_constants():
     assert _abi.state_stride(2, 2) == 98 + 24 + 12
     assert _abi.REWARD_NAMES[_abi.NREWARD - 1] == "body_collision"
+
+
+def test_step_entry_points_reject_null_arguments_without_gpu_work():
+    """pp3_step / pp3_rollout / pp3_rollout_timed validate their arguments before any HIP call."""
+    L = _lib.load()
+    assert L.pp3_step(None, None, None) == 1
+    assert L.pp3_rollout(None, C.c_void_p(16), 0, 4, None, None, None, None) == 1
+    assert b"pp3_rollout" in L.pp3_last_error()
+    ms = C.c_float()
+    assert L.pp3_rollout_timed(None, C.c_void_p(16), 0, 4, None, None, None, C.byref(ms)) == 1
