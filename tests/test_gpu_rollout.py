@@ -128,3 +128,28 @@ def test_rollout_device_stride_zero_and_partial_outputs(require_gpu):
     finally:
         e1.close()
         e2.close()
+
+
+@pytest.mark.parametrize("cap", [8, 16])
+def test_rollout_terrain_pipeline_and_odd_batch(require_gpu, tmp_path, cap):
+    """Both kernel instances (contact cap 8 / 16) with per-env terrain under the robots, the
+    Brax pipeline record on, and an odd env count (the last wave's second half stores nothing)."""
+    n = 65
+    path = common.write_model(tmp_path, 10)
+    kw = dict(num_envs=n, max_contacts=cap, pipeline_output=True)
+    e1, e2 = PupperV3Env(**common.fixture_kwargs(path), **kw), PupperV3Env(**common.fixture_kwargs(path), **kw)
+    acts = np.random.RandomState(4).uniform(-1, 1, size=(6, n, 12)).astype(np.float32)
+    try:
+        s1, s2 = e1.reset(make_keys(15, n)), e2.reset(make_keys(15, n))
+        terrain = common.terrain_under(np.asarray(s1.pipeline_state.q)[:, 0:2], 10, seed=5)
+        e1.set_terrain(terrain)
+        e2.set_terrain(terrain)
+        s1, tr1 = e1.rollout(s1, acts)
+        s2, tr2 = _steps(e2, s2, acts)
+        _check(tr1, tr2, s1, s2)
+        np.testing.assert_array_equal(e1._get(_abi.F_PIPELINE), e2._get(_abi.F_PIPELINE))
+        ncon = e1._get(_abi.F_PIPELINE)[:, _abi.P_NCON]
+        assert ncon.max() > 0
+    finally:
+        e1.close()
+        e2.close()
