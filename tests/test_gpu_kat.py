@@ -4,6 +4,8 @@ Frictionloss (xml:55) on the HIP path: a torque below the threshold gives MuJoCo
 soft-constraint creep v = tau R / (b + damping R) (R = (1 - d)/d * dof_invweight0, d = impedance at
 0, b = 2 / (dmax timeconst)); above it the joint accelerates at (tau - frictionloss - damping v) /
 M_jj.  Tolerances are fp32-sized: 0.5 % on the creep velocity, 1.5 % on the slip acceleration.
+Joint limits: a hinge pushed into its range limit rests where the limit row's soft-constraint
+force equals the torque (test_physics_kat._limit_rest_prediction).
 """
 import numpy as np
 import pytest
@@ -131,3 +133,33 @@ def test_kernel_impratio_scales_the_creep(require_gpu):
         creep[ir] = F._slip(q, v)[0]
     assert creep[1.0] > 0 and creep[10.0] > 0
     assert 5.0 < creep[1.0] / creep[10.0] < 15.0, creep
+
+
+def test_kernel_joint_limit_rest_position(require_gpu):
+    """The kernel's joint-limit rows at rest (test_physics_kat.test_joint_limit_rest_position): a
+    hinge pushed into its range limit settles at the documented soft-limit equilibrium, beyond the
+    solimp width and inside it, against upper and lower limits."""
+    m = K._torque_model()
+    n = len(K.LIMIT_CASES)
+    e = G.env_with_model(common.MODEL_XML, m, n)
+    try:
+        q = np.zeros((n, 19))
+        q[:, 3] = 1
+        q[:, 7:] = K.DP
+        ctrl = np.zeros((n, 12))
+        want = []
+        for i, (jnt, tau) in enumerate(K.LIMIT_CASES):
+            side, x, q_expect = K._limit_rest_prediction(m, jnt, tau)
+            q[i, m.jnt_qposadr[jnt]] = m.jnt_range[jnt][(side + 1) // 2] - side * 0.002
+            ctrl[i, m.jnt_dofadr[jnt] - 6] = tau
+            want.append((jnt, side, x, q_expect))
+        q1, v1, w1, _ = G.gpu_physics(e, q, np.zeros((n, 18)), np.zeros((n, 18)), ctrl, 1500)
+        q2, v2, _, _ = G.gpu_physics(e, q1, v1, w1, ctrl, 1)
+        for i, (jnt, side, x, q_expect) in enumerate(want):
+            a, dof = m.jnt_qposadr[jnt], m.jnt_dofadr[jnt]
+            assert abs(v1[i, dof] + v2[i, dof]) < 1e-5, (jnt, v1[i, dof], v2[i, dof])
+            rng = m.jnt_range[jnt][(side + 1) // 2]
+            got = 0.5 * (q1[i, a] + q2[i, a]) - rng
+            assert abs(got - (q_expect - rng)) <= 3e-3 * abs(x) + 2e-6, (jnt, got, q_expect - rng)
+    finally:
+        e.close()

@@ -328,3 +328,65 @@ def test_resting_robot_carries_its_weight():
     dist = p[_abi.P_CON_DIST:_abi.P_CON_DIST + ncon]
     assert ncon >= 3 and np.all(dist < 0)
     assert np.all(-dist < 0.016), dist
+
+
+# ------------------------------------------------------------------ joint-limit rows at rest
+def _limit_rest_prediction(m, jnt, tau):
+    """Where a hinge pushed by a constant torque tau comes to rest against its limit (MuJoCo's
+    documented soft-constraint model, not either implementation): the side the torque pushes into,
+    and x = pos - margin of that limit row (pos = side (range - q) < 0 when violated).  At rest
+    (a = v = 0) the row force is f = D aref = -(k d(x) / R(x)) x with R = (1 - d)/d * A,
+    A = dof_invweight0, k = 1/(dmax tc dr)^2 (tc >= 2 timestep, REFSAFE); the joint-space balance
+    -side f + tau = 0 gives x = -|tau| A (1 - d(x)) / (k d(x)^2), solved by bisection (d from
+    solimp on |x|)."""
+    side = 1 if tau > 0 else -1
+    dof = m.jnt_dofadr[jnt]
+    si = np.array(m.jnt_solimp[jnt][:])
+    tc, dr = m.jnt_solref[jnt][0], m.jnt_solref[jnt][1]
+    tc = max(tc, 2 * m.timestep)
+    k = 1.0 / (si[1] * tc * dr) ** 2
+    A = m.dof_invweight0[dof]
+
+    def resid(x):
+        d = _imp(si, x)
+        return x + abs(tau) * A * (1 - d) / (k * d * d)
+    lo, hi = -1.0, 0.0  # resid(-1) < 0 < resid(0)
+    for _ in range(200):
+        mid = 0.5 * (lo + hi)
+        if resid(mid) < 0:
+            lo = mid
+        else:
+            hi = mid
+    x = 0.5 * (lo + hi)
+    rng = m.jnt_range[jnt][(side + 1) // 2]
+    # pos = side (rng - q) = x + margin  ->  q = rng - side (x + margin)
+    return side, x, rng - side * (x + m.jnt_margin[jnt])
+
+
+LIMIT_CASES = [(3, 0.3), (3, -0.3), (3, 0.01), (1, -0.25)]  # (joint, torque): knee both sides, in the solimp width, hip
+
+
+@pytest.mark.parametrize("jnt,tau", LIMIT_CASES)
+def test_joint_limit_rest_position(jnt, tau):
+    """A hinge driven into its range limit by a constant torque settles at the documented soft-limit
+    equilibrium: beyond the solimp width (d = dmax) and inside it (d on the sigmoid); the limit row
+    then carries exactly the torque (the frictionloss row carries nothing at rest)."""
+    m = _torque_model()
+    dof = m.jnt_dofadr[jnt]
+    side, x, q_expect = _limit_rest_prediction(m, jnt, tau)
+    assert (abs(x) > m.jnt_solimp[jnt][2]) == (abs(tau) > 0.1)  # the cases cover both impedance zones
+    q = np.zeros(19)
+    q[3] = 1
+    q[7:] = DP
+    q[m.jnt_qposadr[jnt]] = m.jnt_range[jnt][(side + 1) // 2] - side * 0.002  # just inside the limit
+    ctrl = np.zeros(12)
+    ctrl[dof - 6] = tau
+    qn, vn, wn, _, _ = O.mj_step(m, q, np.zeros(18), np.zeros(18), ctrl, nsteps=1500)
+    q2, v2, _, _, _ = O.mj_step(m, qn, vn, wn, ctrl, nsteps=1)
+    # at rest over a substep pair: against a lower limit the folded leg's parent hinges keep a
+    # period-2 chatter (v flips sign every substep; one Newton iteration with the frictionloss rows
+    # at their kinks), which leaves the mean motion and the pushed joint's position at rest
+    assert abs(vn[dof] + v2[dof]) < 1e-8 and np.abs(vn[6:] + v2[6:]).max() < 2e-5, (vn[dof], v2[dof])
+    qa = 0.5 * (qn[m.jnt_qposadr[jnt]] + q2[m.jnt_qposadr[jnt]])
+    rng = m.jnt_range[jnt][(side + 1) // 2]
+    np.testing.assert_allclose(qa - rng, q_expect - rng, rtol=2e-3)
