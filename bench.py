@@ -376,6 +376,8 @@ def main():
                          "lax.scan with the actions given up front; per-step reward/done/obs trajectories written), "
                          "then the same K steps as K single-step launches from the same start state, timed too and "
                          "checked bit-equal; step: K single-step launches only (pp3_step)")
+    ap.add_argument("--no-prewarm", action="store_true",
+                    help="skip the ~200 ms untimed GPU pre-warm (state restored after it) before the warmup steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency-floor", action="store_true",
                     help="skip the E/2-envs latency-floor launches (keeps rocprof stats to E-env launches)")
@@ -467,8 +469,6 @@ def main():
     env.synchronize()
     act_at = lambda i: acts.ptr.value + i * E * 48  # noqa: E731  (actions of step i)
     ms = C.c_float()
-    if args.warmup:
-        _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, args.warmup, C.byref(ms)))
     gather_dst, nmax = None, 0
     if args.gather:
         nmax = E  # equal shards: every rank contributes E rows of width 36H + 2
@@ -495,29 +495,65 @@ def main():
         pol = export.convert_params((norm, {"params": layers}), "elu", 0.75, 5.0, 0.25, np.zeros(12), np.ones(12),
                                     -np.ones(12), True, env._observation_history, 30.0, 30.0)
         policy = export.DevicePolicy(pol, device)
-        for _ in range(args.warmup):
-            policy.act_env(env, acts.ptr.value)
-            env.step_device(acts.ptr.value)
 
     # --launch rollout (the default for the plain env-step workloads): the timed K steps are one
     # fused launch writing per-step trajectories; the start state is kept to replay the same K
     # steps as single-step launches afterwards (timed, and checked bit-equal)
     rollout = args.launch == "rollout" and policy is None and not args.gather
     traj, snap = None, None
-    if rollout:
+    if rollout or policy is not None:
         D = env.observation_size
         traj = [_lib.DeviceBuffer(4 * args.steps * E, device), _lib.DeviceBuffer(4 * args.steps * E, device),
                 _lib.DeviceBuffer(4 * args.steps * E * D, device)]
-        snap_fields = [_abi.F_STATE, _abi.F_OBS, _abi.F_REWARD, _abi.F_DONE] + ([_abi.F_EPISODE] if args.auto_reset else [])
-        snap = {f: env._get(f) for f in snap_fields}
+    # device-side snapshots of the env's state buffers (D2D copies queued on the env's stream, no
+    # host round trip): the pre-warm and the single-step replay restore them
+    snap_fields = [_abi.F_STATE, _abi.F_OBS, _abi.F_REWARD, _abi.F_DONE] + ([_abi.F_EPISODE] if args.auto_reset else [])
+    stream = L.pp3_stream(env._h)
+
+    def dev_snapshot(bufs=None):
+        bufs = bufs or {f: _lib.DeviceBuffer(4 * E * env.device_field(f)[1], device) for f in snap_fields}
+        for f, b in bufs.items():
+            _lib.check(L.pp3_memcpy_d2d(b.ptr, C.c_void_p(env.device_field(f)[0]), b.nbytes, stream))
+        return bufs
+
+    def dev_restore(bufs):
+        env._before_launch()
+        for f, b in bufs.items():
+            _lib.check(L.pp3_memcpy_d2d(C.c_void_p(env.device_field(f)[0]), b.ptr, b.nbytes, stream))
+
+    # GPU pre-warm (untimed; the env's state is restored afterwards): ~200 ms of the same launches,
+    # so the timed window runs at the clocks of a busy GPU.  After a host-side pause of 0.2 s the
+    # same 20-step window measured 6-7 % slower than right after continuous work;
+    # a training loop keeps the GPU busy.  --no-prewarm measures from the idle state.
+    prewarm_ms = 0.0
+    if not args.no_prewarm:
+        s0 = dev_snapshot()
+        t_pw = time.perf_counter()
+        n_pw = 0
+        while time.perf_counter() - t_pw < 0.2:
+            _lib.check(L.pp3_rollout(env._h, acts.ptr, E * 12, min(total, 20), None, None, None, None))
+            dev_restore(s0)
+            n_pw += 1
+            if n_pw % 4 == 0:
+                env.synchronize()
+        prewarm_ms = (time.perf_counter() - t_pw) * 1e3
+    # the W untimed warmup steps, right before the timed window
+    if args.warmup:
+        if policy is not None:
+            _lib.check(L.pp3_rollout_policy(env._h, policy._h, args.warmup, acts.ptr, None, None, None, None))
+        else:
+            _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, args.warmup, C.byref(ms)))
+    if rollout:
+        snap = dev_snapshot()  # the timed window's start state
 
     env.synchronize()
     barrier()
     t0 = time.perf_counter()
     if policy is not None:
-        for i in range(args.steps):
-            policy.act_env(env, acts.ptr.value)
-            env.step_device(acts.ptr.value)
+        # generate_unroll with the policy in the loop: pp3_rollout_policy (per step the MLP on the
+        # obs buffer, then the env step; action / reward / done / obs trajectories written)
+        _lib.check(L.pp3_rollout_policy(env._h, policy._h, args.steps, C.c_void_p(act_at(args.warmup)),
+                                        traj[0].ptr, traj[1].ptr, traj[2].ptr, None))
         env.synchronize()
         kernel_ms = (time.perf_counter() - t0) * 1e3  # policy + env step per iteration (no per-kernel events)
     elif not args.gather and rollout:
@@ -536,30 +572,30 @@ def main():
     env.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    # the rollout's end state (rank 0's shard): equal hashes across kernel builds mean the A/B
-    # variants ran the same trajectories, so a timing difference is code speed, not a changed workload
-    import hashlib
-    state_sha16 = hashlib.sha256(env._get(_abi.F_STATE).tobytes()).hexdigest()[:16]
     per_step = None
     if rollout:
-        # untimed by the wall clock: the trajectories' last row against the handle's outputs, then
-        # the same K steps again as K single-step launches (HIP events) from the kept start state
+        # the same K steps again as K single-step launches (HIP events) from the kept start state,
+        # queued right behind the timed window (the rollout's end state kept on the device first)
         K, D = args.steps, env.observation_size
+        end_dev = dev_snapshot()
+        dev_restore(snap)
+        _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, K, C.byref(ms)))
+        step_ms = ms.value
+        end = {f: np.empty((E, env.device_field(f)[1]), np.float32) for f in snap_fields}
+        for f, a in end.items():
+            end_dev[f].download(a)
+        # the trajectories' last row against the rollout's outputs
         last_r, last_d, last_o = np.empty(E, np.float32), np.empty(E, np.float32), np.empty(E * D, np.float32)
         _lib.check(L.pp3_memcpy_d2h(last_r.ctypes.data_as(C.c_void_p), C.c_void_p(traj[0].ptr.value + 4 * (K - 1) * E), 4 * E))
         _lib.check(L.pp3_memcpy_d2h(last_d.ctypes.data_as(C.c_void_p), C.c_void_p(traj[1].ptr.value + 4 * (K - 1) * E), 4 * E))
         _lib.check(L.pp3_memcpy_d2h(last_o.ctypes.data_as(C.c_void_p), C.c_void_p(traj[2].ptr.value + 4 * (K - 1) * E * D), 4 * E * D))
-        traj_ok = (np.array_equal(last_r, env._get(_abi.F_REWARD)[:, 0]) and np.array_equal(last_d, env._get(_abi.F_DONE)[:, 0])
-                   and np.array_equal(last_o.reshape(E, D), env._get(_abi.F_OBS)))
-        end = {f: env._get(f) for f in snap}
-        for f, v in snap.items():
-            env._put(f, v)
-        env.synchronize()
-        _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, K, C.byref(ms)))
-        step_ms = ms.value
+        traj_ok = (np.array_equal(last_r, end[_abi.F_REWARD][:, 0]) and np.array_equal(last_d, end[_abi.F_DONE][:, 0])
+                   and np.array_equal(last_o.reshape(E, D), end[_abi.F_OBS]))
         # bitwise (the state record holds the rng key words as float bit patterns, some of them NaNs)
         differ = [int(f) for f, v in end.items() if not np.array_equal(env._get(f).view(np.uint32), v.view(np.uint32))]
         same = not differ
+        for b in list(end_dev.values()) + list(snap.values()):
+            b.free()
         per_step = {"launches": K, "avg_launch_ms": round(step_ms / K, 4),
                     "kernel_env_steps_per_s": round(E * K / (step_ms / 1e3), 1),
                     "bit_equal_to_rollout": bool(same), "trajectory_last_row_equals_outputs": bool(traj_ok)}
@@ -569,6 +605,11 @@ def main():
             print(f"rank {rank}: fused rollout differs from single-step launches: {per_step}", file=sys.stderr, flush=True)
         for b in traj:
             b.free()
+    # the timed window's end state (rank 0's shard; after the replay when it is bit-equal): equal
+    # hashes across kernel builds mean the A/B variants ran the same trajectories, so a timing
+    # difference is code speed, not a changed workload
+    import hashlib
+    state_sha16 = hashlib.sha256((end[_abi.F_STATE] if rollout else env._get(_abi.F_STATE)).tobytes()).hexdigest()[:16]
     gather_info = None
     if args.gather:
         # untimed: the same K steps' kernels alone (events), then the gather alone
@@ -634,6 +675,7 @@ def main():
             "n_gpus": n_gpus,
             "steps": K,
             "warmup": args.warmup,
+            "gpu_prewarm_ms": round(prewarm_ms, 1),
             "ms_per_step": round(wall_max / K * 1e3, 4),
             "state_sha16": state_sha16,
             "higher_is_better": True,
@@ -655,7 +697,10 @@ def main():
                        "policy_in_loop": args.policy or None},
             "launch": (f"rollout: the {K} timed steps fused into one pp3_rollout launch (per-step reward/done/obs "
                        "trajectories written); per_step_launch = the same steps as single-step launches"
-                       if rollout else "step: one pp3_step launch per env step"),
+                       if rollout else
+                       ("policy: pp3_rollout_policy, per step the MLP launch on the obs buffer then the env step "
+                        "(action/reward/done/obs trajectories written), one C call for the K steps"
+                        if policy is not None else "step: one pp3_step launch per env step")),
             "per_step_launch": per_step,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,

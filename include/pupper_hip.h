@@ -485,6 +485,14 @@ int pp3_policy_act(pp3_policy_t* policy, const float* obs_dev, int64_t obs_strid
                    float* actions_dev, int64_t action_stride, void* stream);
 int pp3_policy_out_dim(const pp3_policy_t* policy);
 int pp3_policy_destroy(pp3_policy_t* policy);
+/* The unroll of brax's generate_unroll with the policy in the loop ([ext] brax 0.12.1
+ * training/acting.py: actions = policy(obs), state = env.step(state, actions), nsteps times), on the
+ * env's stream with no host round trip: step t launches the policy on the env's observation buffer,
+ * writing actions_dev + t * N * 12 (f32[nsteps][N][12], required: the trajectory's actions), then
+ * the env step on them; reward / done / obs trajectories as pp3_rollout (optional).  The policy must
+ * have 12 outputs and 36H inputs and live on the env's device. */
+int pp3_rollout_policy(pp3_env_t* env, pp3_policy_t* policy, int32_t nsteps, float* actions_dev,
+                       float* reward_dev, float* done_dev, float* obs_dev, void* stream);
 const char* pp3_policy_last_error(void);
 
 /* ---------------------------------------------------------------------------------------

@@ -3361,6 +3361,26 @@ int pp3_rollout(pp3_env_t* e, const float* actions_dev, int64_t action_stride, i
   return launch_steps(e, actions_dev, action_stride, nsteps, reward_dev, done_dev, obs_dev, true, stream);
 }
 
+int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float* actions_dev, float* reward_dev,
+                       float* done_dev, float* obs_dev, void* stream) {
+  if (!e || !policy || !actions_dev) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: null argument");
+  if (nsteps < 1) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: nsteps must be >= 1");
+  if (pp3_policy_out_dim(policy) != NU) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: the policy must have 12 outputs");
+  const size_t on = (size_t)e->N * PP3_OBS_DIM * e->H;
+  const hipStream_t st = stream_of(e, stream);
+  for (int t = 0; t < nsteps; t++) {
+    float* act = actions_dev + (size_t)t * e->N * NU;
+    if (pp3_policy_act(policy, e->obs, PP3_OBS_DIM * e->H, e->N, act, NU, (void*)st) != PP3_OK)
+      return set_err(PP3_ERR_ARG, std::string("pp3_rollout_policy: ") + pp3_policy_last_error());
+    // one single-step launch of the rollout kernel: it writes this step's trajectory rows
+    const int rc = launch_steps(e, act, 0, 1, reward_dev ? reward_dev + (size_t)t * e->N : nullptr,
+                                done_dev ? done_dev + (size_t)t * e->N : nullptr, obs_dev ? obs_dev + (size_t)t * on : nullptr,
+                                true, (void*)st);
+    if (rc) return rc;
+  }
+  return PP3_OK;
+}
+
 void* pp3_stream(pp3_env_t* e) { return e ? (void*)e->stream : nullptr; }
 
 int pp3_set_auto_reset(pp3_env_t* e, int32_t episode_length) {

@@ -72,6 +72,7 @@ def load() -> C.CDLL:
     L.pp3_policy_act.argtypes = [vp, vp, i64, i32, vp, i64, vp]
     L.pp3_policy_out_dim.argtypes = [vp]
     L.pp3_policy_destroy.argtypes = [vp]
+    L.pp3_rollout_policy.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
     L.pp3_policy_last_error.restype = C.c_char_p
     L.pp3_stream.argtypes = [vp]
     L.pp3_stream.restype = vp
@@ -98,7 +99,7 @@ def load() -> C.CDLL:
                  "pp3_memcpy_h2d_async",
                  "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
                  "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
-                 "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy",
+                 "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy", "pp3_rollout_policy",
                  "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
                  "pp3_comm_allreduce", "pp3_comm_barrier", "pp3_render"):
         getattr(L, name).restype = C.c_int
@@ -130,6 +131,7 @@ EXPORTED_SYMBOLS = (
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
     "pp3_fill_uniform", "pp3_step_timed", "pp3_rollout_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
+    "pp3_rollout_policy",
     "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
     "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_comm_rank", "pp3_comm_world",
     "pp3_comm_last_error", "pp3_gather", "pp3_comm_allreduce", "pp3_comm_barrier",

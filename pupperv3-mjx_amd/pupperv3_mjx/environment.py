@@ -565,6 +565,31 @@ class PupperV3Env:
             traj = {k: v[:, 0] for k, v in traj.items()}
         return self._issue(single), traj
 
+    def rollout_policy(self, state: State, policy, nsteps: int) -> Tuple[State, Dict[str, np.ndarray]]:
+        """brax's generate_unroll with the policy in the loop, on device (pp3_rollout_policy):
+        `policy` (an `export.DevicePolicy` with 12 outputs) acts on the env's observation buffer
+        before each of the `nsteps` steps; no host round trip until the end.  Returns the state
+        after the last step and {"obs": [K, N, 36H], "action": [K, N, 12], "reward": [K, N],
+        "done": [K, N]} (single-env states: without the N axis)."""
+        single = np.ndim(state.reward) == 0
+        n, D, K = self.num_envs, self.observation_size, int(nsteps)
+        if K < 1:
+            raise ValueError("nsteps must be >= 1")
+        if not self.holds(state):
+            self._write_state(state)
+        bufs = self._rollout_buffers(K)
+        self._before_launch()
+        _lib.check(self._L.pp3_rollout_policy(self._h, policy._h, K, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr,
+                                              bufs[3].ptr, None))
+        self.synchronize()
+        traj = {"obs": np.empty((K, n, D), np.float32), "action": np.empty((K, n, _abi.NU), np.float32),
+                "reward": np.empty((K, n), np.float32), "done": np.empty((K, n), np.float32)}
+        for b, k in zip(bufs, ("action", "reward", "done", "obs")):
+            b.download(traj[k])
+        if single:
+            traj = {k: v[:, 0] for k, v in traj.items()}
+        return self._issue(single), traj
+
     def _rollout_buffers(self, K: int) -> list:
         """Device buffers of rollout(): actions, reward, done, obs for K steps (kept and grown)."""
         cur = getattr(self, "_roll_bufs", None)

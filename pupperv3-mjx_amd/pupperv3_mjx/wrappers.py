@@ -98,6 +98,11 @@ class AutoResetEpisodeEnv:
         self._prepare(state)
         return self.env.rollout(state, actions)
 
+    def rollout_policy(self, state: State, policy, nsteps: int):
+        """K wrapper steps with the on-device policy in the loop (PupperV3Env.rollout_policy)."""
+        self._prepare(state)
+        return self.env.rollout_policy(state, policy, nsteps)
+
     def _prepare(self, state: State) -> None:
         n = self.env.num_envs
         if not self.env.holds(state):

@@ -61,3 +61,37 @@ def test_policy_env_rollout_on_device(require_gpu, tmp_path):
         assert np.all(np.isfinite(e._get(_abi.F_OBS))) and np.all(np.isfinite(e._get(_abi.F_REWARD)))
     finally:
         ab.free(); dp.close(); e.close()
+
+
+def test_rollout_policy_equals_act_then_step(require_gpu, tmp_path):
+    """pp3_rollout_policy (policy in the loop, one C call for K steps, trajectories written) equals
+    the Python loop DevicePolicy.act_env + step, bit for bit, with auto-reset inside the window."""
+    from pupperv3_mjx import wrappers
+    path = common.write_model(tmp_path, 0)
+    n, K = 48, 12
+    envs = [PupperV3Env(**common.fixture_kwargs(path, terminal_body_z=0.25), num_envs=n) for _ in range(2)]
+    pol = _policy([72, 128, 128, 24], "elu")
+    dp = export.DevicePolicy(pol)
+    ab = _lib.DeviceBuffer(n * 12 * 4)
+    try:
+        ws = [wrappers.wrap(e, episode_length=5) for e in envs]
+        s1, s2 = ws[0].reset(make_keys(2, n)), ws[1].reset(make_keys(2, n))
+        s1, tr = ws[0].rollout_policy(s1, dp, K)
+        acts, obs, rew, done = [], [], [], []
+        for _ in range(K):
+            dp.act_env(envs[1], ab.ptr.value)
+            a = np.zeros((n, 12), dtype=np.float32)
+            envs[1].synchronize()
+            _lib.check(_lib.load().pp3_memcpy_d2h(a.ctypes.data_as(C.c_void_p), ab.ptr, a.nbytes))
+            s2 = ws[1].step(s2, a)
+            acts.append(a); obs.append(np.array(s2.obs)); rew.append(np.array(s2.reward)); done.append(np.array(s2.done))
+        np.testing.assert_array_equal(tr["action"], np.stack(acts))
+        np.testing.assert_array_equal(tr["obs"], np.stack(obs))
+        np.testing.assert_array_equal(tr["reward"], np.stack(rew))
+        np.testing.assert_array_equal(tr["done"], np.stack(done))
+        assert tr["done"].sum() > 0
+        np.testing.assert_array_equal(s1._record, s2._record)
+    finally:
+        ab.free(); dp.close()
+        for e in envs:
+            e.close()

@@ -32,13 +32,37 @@ def _kernel():
 
 
 def _pmc(d):
+    """Counters of the summarised kernel: for the fused rollout the LAST dispatch of
+    env_step_kernel<8, true> (the timed window; the bench's untimed GPU pre-warm launches the same
+    kernel for 20-step rollouts before it), for single-step launches the mean over dispatches."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-    agg = defaultdict(list)
+    per = defaultdict(lambda: defaultdict(float))
     for f in files:
         for r in csv.DictReader(open(f)):
             if _kernel() in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    if not per:
+        return {}
+    if _arg("--launch", "rollout") == "rollout":
+        return dict(per[max(per)])
+    agg = defaultdict(list)
+    for c in per.values():
+        for k, v in c.items():
+            agg[k].append(v)
     return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def _trace_last(d):
+    """Duration (ns) of the last dispatch of the summarised kernel in the kernel trace."""
+    files = glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    last = None
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if _kernel() in r["Kernel_Name"]:
+                did = int(r["Dispatch_Id"])
+                if last is None or did > last[0]:
+                    last = (did, int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return None if last is None else float(last[1])
 
 
 def main():
@@ -52,6 +76,11 @@ def main():
             if _kernel() in r["Name"]:
                 out["kernel_avg_ns"] = float(r["AverageNs"])
                 out["kernel_calls"] = int(r["Calls"])
+    if launch == "rollout":
+        t = _trace_last(d)
+        if t is not None:  # the timed window's launch (the stats' average includes the pre-warm's)
+            out["kernel_avg_ns"] = t
+            out["timed_launch_ns"] = t
     sq = _pmc(os.path.join(d, "pmc_sq"))
     if sq:
         waves = sq.get("SQ_WAVES", 1.0)
@@ -71,6 +100,13 @@ def main():
         dst = sys.argv[sys.argv.index("--commit") + 1]
         if stats:
             shutil.copy(stats[0], dst + "_kernel_stats.csv")
+        traces = glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True)
+        if traces:  # every env_step_kernel dispatch: the pre-warm's, the timed window's, the replay's
+            with open(dst + "_env_step_dispatches.csv", "w") as fo:
+                fo.write("dispatch_id,kernel,duration_ns\n")
+                for r in csv.DictReader(open(traces[0])):
+                    if "env_step_kernel" in r["Kernel_Name"]:
+                        fo.write(f'{r["Dispatch_Id"]},"{r["Kernel_Name"]}",{int(r["End_Timestamp"]) - int(r["Start_Timestamp"])}\n')
         json.dump(out, open(dst + "_pmc_summary.json", "w"), indent=1)
         # the bench's roofline.traffic / valu_issue source, keyed to the kernel sources it was measured on
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
