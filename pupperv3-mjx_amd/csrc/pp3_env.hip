@@ -2163,6 +2163,7 @@ template <int NC, bool FUSED>
 __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   __shared__ Shared<NC> sh[2];
   const int nsteps = FUSED ? a_arg.nsteps : 1;
+  constexpr bool TG = true;  // trajectory rows (optional pointers) written by both kernels: free in the single-step one
 #ifdef PP3_PHASE_PROF
   const uint32_t t_start_ = shader_cycles();
   const uint32_t rt_start_ = (uint32_t)__builtin_amdgcn_s_memrealtime();  // 100 MHz, chip-wide
@@ -2192,7 +2193,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;
   // fused rollout: this step's observation row of the trajectory (optional)
-  float* const to = FUSED && a.traj_obs ? a.traj_obs + ((size_t)it * a.N + env) * (PP3_OBS_DIM * m.H) : nullptr;
+  float* const to = TG && a.traj_obs ? a.traj_obs + ((size_t)it * a.N + env) * (PP3_OBS_DIM * m.H) : nullptr;
   // ---- every global load of this env step issued together (one memory round trip): state
   // record head, this lane's action-latency row and IMU row, the action, the obs history, the
   // lane's env constants and body parameters; the global stores only after all of them ----
@@ -2241,7 +2242,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
     for (int t = 0; t < OBS_MOVE; t++)
       if (l + HW * t < nmove) {
         oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
-        if (FUSED && to) to[PP3_OBS_DIM + l + HW * t] = tmp[t];
+        if (TG && to) to[PP3_OBS_DIM + l + HW * t] = tmp[t];
       }
 #pragma unroll
   for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
@@ -2334,7 +2335,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
     if (own)
       for (int k = l; k < PP3_OBS_DIM; k += HW) {
         oo[k] = s.x.e.o[k];
-        if (FUSED && to) to[k] = s.x.e.o[k];
+        if (TG && to) to[k] = s.x.e.o[k];
       }
   }
   SYNC();
@@ -2482,7 +2483,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   if (own && l == 0) {
     a.reward[env] = rout;
     if (!a.episode || last) a.done[env] = done_out ? 1.0f : 0.0f;
-    if (FUSED && (!a.episode || last)) {
+    if (TG && (!a.episode || last)) {
       if (a.traj_reward) a.traj_reward[(size_t)it * a.N + env] = rout;
       if (a.traj_done) a.traj_done[(size_t)it * a.N + env] = done_out ? 1.0f : 0.0f;
     }
@@ -2504,7 +2505,8 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   }
   if (isdone || resample) stepc = 0;
   if (l == 0) s.st[PP3_S_STEP] = (float)stepc;
-  if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
+  // the Brax pipeline record is the returned state's: a fused rollout writes it at its last step only
+  if (own && a.pipe && (!FUSED || it == nsteps - 1)) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
   if (a.episode && last && done_out) {  // AutoResetWrapper: pipeline state and obs <- the reset's
     const float* fs = a.first_state + (size_t)env * PP3_FIRST_STRIDE;
     for (int i = l; i < PP3_FIRST_STRIDE; i += HW) s.st[PP3_S_QPOS + i] = fs[i];
@@ -2513,7 +2515,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
     if (own)
       for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) {
         oo[i] = fo[i];
-        if (FUSED && to) to[i] = fo[i];
+        if (TG && to) to[i] = fo[i];
       }
   }
   SYNC();
@@ -3324,6 +3326,9 @@ static int launch_steps(pp3_env_t* e, const float* actions_dev, int64_t action_s
   a.N = e->N;
   a.repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;
   a.act_stride = action_stride;
+  // a one-step rollout takes the single-step kernel: a fused launch of one step measured 7 % slower
+  // than it (the fused kernel only pays off across steps)
+  if (nsteps == 1) fused = false;
   const bool one_launch = fused && a.repeat == 1;
   a.nsteps = one_launch ? nsteps : 1;
   const dim3 grid((e->N + 1) / 2), block(WAVE);
@@ -3372,10 +3377,10 @@ int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float
     float* act = actions_dev + (size_t)t * e->N * NU;
     if (pp3_policy_act(policy, e->obs, PP3_OBS_DIM * e->H, e->N, act, NU, (void*)st) != PP3_OK)
       return set_err(PP3_ERR_ARG, std::string("pp3_rollout_policy: ") + pp3_policy_last_error());
-    // one single-step launch of the rollout kernel: it writes this step's trajectory rows
+    // one single-step launch; it writes this step's trajectory rows
     const int rc = launch_steps(e, act, 0, 1, reward_dev ? reward_dev + (size_t)t * e->N : nullptr,
                                 done_dev ? done_dev + (size_t)t * e->N : nullptr, obs_dev ? obs_dev + (size_t)t * on : nullptr,
-                                true, (void*)st);
+                                false, (void*)st);
     if (rc) return rc;
   }
   return PP3_OK;
