@@ -153,3 +153,21 @@ def test_rollout_terrain_pipeline_and_odd_batch(require_gpu, tmp_path, cap):
     finally:
         e1.close()
         e2.close()
+
+
+def test_rollout_long_history_and_latency_buffers(require_gpu):
+    """H = 15 (the history window shifts over itself in place, read back across fused steps) with
+    4-long action and 3-long IMU latency buffers."""
+    kw = common.fixture_kwargs(MODEL_XML, observation_history=15, latency_distribution=[0.1, 0.2, 0.3, 0.4],
+                               imu_latency_distribution=[0.2, 0.3, 0.5])
+    e1, e2 = PupperV3Env(**kw, num_envs=N), PupperV3Env(**kw, num_envs=N)
+    acts = np.random.RandomState(5).uniform(-1, 1, size=(18, N, 12)).astype(np.float32)
+    try:
+        s1, s2 = e1.reset(make_keys(16, N)), e2.reset(make_keys(16, N))
+        assert s1.obs.shape == (N, 36 * 15)
+        s1, tr1 = e1.rollout(s1, acts)
+        s2, tr2 = _steps(e2, s2, acts)
+        _check(tr1, tr2, s1, s2)
+    finally:
+        e1.close()
+        e2.close()
