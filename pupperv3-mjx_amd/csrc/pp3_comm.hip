@@ -53,7 +53,21 @@ Rccl g_rccl;
 std::string g_rccl_err;
 void load_rccl() {
   Rccl& r = g_rccl;
+#ifdef PP3_TEST_RCCL_SONAME
+  // test build only (`make loopback` -> tests/loopback/, never the product library): the RCCL API
+  // of the loopback test transport built next to this library (several rank processes on one
+  // GPU, which RCCL refuses); pp3_create refuses this build unless the caller opts in (pp3_diag.h)
+  Dl_info self;
+  std::string path = PP3_TEST_RCCL_SONAME;
+  if (dladdr((const void*)&load_rccl, &self) && self.dli_fname) {
+    const std::string me = self.dli_fname;
+    const size_t cut = me.rfind('/');
+    if (cut != std::string::npos) path = me.substr(0, cut + 1) + PP3_TEST_RCCL_SONAME;
+  }
+  const char* names[] = {path.c_str()};
+#else
   const char* names[] = {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
+#endif
   for (const char* n : names)
     if ((r.so = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
   if (!r.so) {

@@ -3,11 +3,13 @@
 // The product target (`make`, libpupper_hip.so) defines none of the macros below, so every hook
 // compiles to nothing.  `make prof` (-DPP3_PHASE_PROF -> libpupper_hip_prof.so) and `make debug`
 // (-DPP3_DEBUG -> libpupper_hip_dbg.so) build separate libraries for tests/diag_*.py and the
-// tools/ scripts; pp3_create refuses to run from a diagnostic build unless the caller opts in
-// with PP3_ALLOW_DIAG_BUILD=1 (pp3_env.hip), so a stray -D can never pass for the product.
+// tools/ scripts, and `make loopback` (-DPP3_TEST_RCCL_SONAME -> tests/loopback/) the multi-rank
+// test build whose collectives go through the loopback test transport; pp3_create refuses to run
+// from any of them unless the caller opts in with PP3_ALLOW_DIAG_BUILD=1 (pp3_env.hip), so a
+// stray -D can never pass for the product.
 #pragma once
 
-#if defined(PP3_PHASE_PROF) || defined(PP3_DEBUG)
+#if defined(PP3_PHASE_PROF) || defined(PP3_DEBUG) || defined(PP3_TEST_RCCL_SONAME)
 #define PP3_DIAG_BUILD 1
 #else
 #define PP3_DIAG_BUILD 0

@@ -1,7 +1,10 @@
-"""One rank of tests/test_gpu_comm.py::test_two_rank_gather_on_two_devices (not a test module):
-  python tests/_comm_worker.py RANK WORLD OUTDIR
-Rank r steps its shard of a 9-env global batch (ragged: 5 + 4) on device r, then gathers the
-learner rows to root 0 and all-gathers them; it saves its own pack_rows and what it received."""
+"""One rank of tests/test_gpu_comm.py::test_two_rank_gather_on_two_devices and
+tests/test_gpu_multirank.py (not a test module):
+  python tests/_comm_worker.py RANK WORLD OUTDIR [GLOBAL_ENVS]
+Rank r steps its shard of a global batch (default 9 envs: ragged, 5 + 4 on two ranks) on device r
+(PP3_WORKER_DEVICE: every rank on that device -- the loopback transport's one-GPU runs), then
+gathers the learner rows to root 0 and all-gathers them; it saves its own pack_rows and what it
+received."""
 import os
 import sys
 
@@ -14,11 +17,12 @@ from pupperv3_mjx import _lib, sharding  # noqa: E402
 from pupperv3_mjx.environment import PupperV3Env  # noqa: E402
 
 rank, world, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
-G = 9
+G = int(sys.argv[4]) if len(sys.argv) > 4 else 9
+device = int(os.environ.get("PP3_WORKER_DEVICE", rank))
 start, n = sharding.shard_bounds(G, world, rank)
 nmax = sharding.max_shard(G, world)
-comm = sharding.Comm(rank, world, rank)
-env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=n, device=rank)
+comm = sharding.Comm(rank, world, device)
+env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=n, device=device)
 st = env.reset(sharding.shard_keys(5, G, world, rank))
 acts = np.random.RandomState(2).uniform(-1, 1, size=(G, 12)).astype(np.float32)[start:start + n]
 st = env.step(st, acts)

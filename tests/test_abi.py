@@ -62,3 +62,20 @@ def test_step_entry_points_reject_null_arguments_without_gpu_work():
     assert b"pp3_rollout" in L.pp3_last_error()
     ms = C.c_float()
     assert L.pp3_rollout_timed(None, C.c_void_p(16), 0, 4, None, None, None, C.byref(ms)) == 1
+
+
+def test_loopback_transport_exports_the_rccl_api():
+    """The multi-rank test transport (tests/loopback, test_gpu_multirank.py) provides every RCCL
+    entry point pp3_comm.hip binds, and the test build of the library is a separate file that
+    refuses pp3_create without the diagnostic opt-in (pp3_diag.h)."""
+    import ctypes as C
+    here = os.path.dirname(os.path.abspath(__file__))
+    lb = os.path.join(here, "loopback", "libpp3_loopback_rccl.so")
+    if not os.path.exists(lb):
+        pytest.skip("loopback test build absent (make -C pupperv3-mjx_amd/csrc loopback)")
+    T = C.CDLL(lb)
+    for name in ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclAllGather", "ncclAllReduce",
+                 "ncclSend", "ncclRecv", "ncclGroupStart", "ncclGroupEnd", "ncclGetErrorString"):
+        assert hasattr(T, name), name
+    src = open(os.path.join(here, "..", "pupperv3-mjx_amd", "csrc", "pp3_comm.hip")).read()
+    assert "#ifdef PP3_TEST_RCCL_SONAME" in src  # the product build always loads librccl

@@ -6,9 +6,10 @@ a root and for the all-gather; the reductions the bench's max-over-ranks timing 
 return their inputs.  Several ranks need several GPUs (RCCL allows one rank per device):
 test_two_rank_gather_on_two_devices runs the grouped send/recv and the all-gather across two
 processes when the box has two devices and is skipped otherwise; the N > 1 path also runs, with
-its checksum check, in every multi-GPU bench (bench.py gather_check).  Until one of those has run
-on hardware, the multi-rank exchange is unverified on hardware (the gloo test in
-test_sharding.py covers its host-side layout).
+its checksum check, in every multi-GPU bench (bench.py gather_check).  On the one-GPU pool,
+test_gpu_multirank.py runs 2 and 3 rank processes through the same code above RCCL (the
+loopback test transport); RCCL's own transport between devices stays unverified until a
+multi-GPU node runs one of the above.
 """
 import ctypes as C
 import os
