@@ -110,3 +110,26 @@ def test_bench_per_step_gather(loopback_env, root):
     g = d["config"]["gather"]
     assert g["root"] == root and g["rows_per_rank"] == 512 and g["ms_per_gather"] > 0
     assert d["config"]["gather_check"]["failing_receivers"] == 0
+
+
+def test_bench_under_torch_distributed_run(loopback_env):
+    """The driver's multi-GPU command: `python -m torch.distributed.run --nnodes=1 --nproc-per-node 2
+    --master-addr 127.0.0.1 --master-port P bench.py --gpus 2 ...` -- the launcher sets RANK /
+    LOCAL_RANK / WORLD_SIZE, the ranks find each other through the launch key of their shared
+    parent (sharding.launch_key) and report one JSON line."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in loopback_env.items() if k != "PP3_LAUNCH_ID"}  # keyed by the launcher
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--envs", "256", "--no-cpu-baseline", "--no-latency-floor", "--no-extras", "--no-prewarm"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["comm"] == "RCCL (pp3_comm)"
+    assert d["config"]["gather_check"]["failing_receivers"] == 0
