@@ -410,6 +410,15 @@ int pp3_synchronize(pp3_env_t* env);
  * pair it with pp3_synchronize).  Meant for page-locked host memory (pp3_host_malloc), which is
  * what lets it run at PCIe speed without a staging copy (the host API's per-step outputs). */
 int pp3_copy_field_to_host_async(pp3_env_t* env, int32_t field, void* host, size_t bytes);
+/* The host API's per-step outputs in one go (environment.py:348 `step` returns State.obs /
+ * .reward / .done): a kernel on the handle's stream stores [obs N x 36H | reward N | done N] straight
+ * into `host`, page-locked memory from pp3_host_malloc of at least N * (36H + 2) floats, through its
+ * device mapping (no copy-engine transfer).  No synchronisation: pair it with pp3_synchronize. */
+int pp3_outputs_to_host(pp3_env_t* env, float* host);
+/* The device address of page-locked host memory from pp3_host_malloc, e.g. to pass a host block as
+ * pp3_rollout's trajectory outputs so the step kernel stores its rows straight into host memory
+ * (the host API's step). */
+int pp3_host_device_ptr(void* host, void** dev_ptr);
 /* The handle's own HIP stream (hipStream_t), for ordering other work (e.g. pp3_policy_act) with it. */
 void* pp3_stream(pp3_env_t* env);
 

@@ -3565,6 +3565,38 @@ int pp3_copy_field_to_host_async(pp3_env_t* e, int32_t field, void* host, size_t
   return PP3_OK;
 }
 
+// obs | reward | done -> one page-locked host block, stored by the CUs through its device mapping
+// (PCIe writes from the kernel; a copy-engine transfer of the same 1.2 MB measured slower)
+__global__ void outputs_to_host_kernel(const float* __restrict__ obs, const float* __restrict__ rew,
+                                       const float* __restrict__ done, int64_t nobs, int n, float* host) {
+  const int64_t total = nobs + 2 * (int64_t)n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+    host[i] = i < nobs ? obs[i] : (i < nobs + n ? rew[i - nobs] : done[i - nobs - n]);
+}
+
+int pp3_outputs_to_host(pp3_env_t* e, float* host) {
+  if (!e || !host) return set_err(PP3_ERR_ARG, "pp3_outputs_to_host: null argument");
+  HIPCHK(hipSetDevice(e->device));
+  float* hdev = nullptr;
+  if (hipHostGetDevicePointer((void**)&hdev, host, 0) != hipSuccess || !hdev)
+    return set_err(PP3_ERR_ARG, "pp3_outputs_to_host: host block is not page-locked memory from pp3_host_malloc");
+  const int64_t nobs = (int64_t)e->N * PP3_OBS_DIM * e->H;
+  const int64_t total = nobs + 2 * (int64_t)e->N;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 1024);
+  hipLaunchKernelGGL(outputs_to_host_kernel, dim3(blocks), dim3(256), 0, e->stream, e->obs, e->reward, e->done, nobs,
+                     e->N, hdev);
+  HIPCHK(hipGetLastError());
+  return PP3_OK;
+}
+
+int pp3_host_device_ptr(void* host, void** dev) {
+  if (!host || !dev) return set_err(PP3_ERR_ARG, "pp3_host_device_ptr: null argument");
+  *dev = nullptr;
+  if (hipHostGetDevicePointer(dev, host, 0) != hipSuccess || !*dev)
+    return set_err(PP3_ERR_ARG, "pp3_host_device_ptr: not page-locked memory from pp3_host_malloc");
+  return PP3_OK;
+}
+
 int pp3_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
   HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
   return PP3_OK;

@@ -60,6 +60,8 @@ def load() -> C.CDLL:
     L.pp3_device_free.argtypes = [vp]
     L.pp3_memcpy_h2d.argtypes = [vp, vp, sz]
     L.pp3_memcpy_d2h.argtypes = [vp, vp, sz]
+    L.pp3_outputs_to_host.argtypes = [vp, vp]
+    L.pp3_host_device_ptr.argtypes = [vp, C.POINTER(vp)]
     L.pp3_memcpy_d2d.argtypes = [vp, vp, sz, vp]
     L.pp3_fill_uniform.argtypes = [vp, vp, i64, C.c_uint32, C.c_uint32, C.c_float, C.c_float, vp]
     L.pp3_step_timed.argtypes = [vp, vp, i64, i32, C.POINTER(C.c_float)]
@@ -98,7 +100,7 @@ def load() -> C.CDLL:
                  "pp3_synchronize", "pp3_copy_field_to_host_async", "pp3_host_malloc", "pp3_host_free",
                  "pp3_memcpy_h2d_async",
                  "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
-                 "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
+                 "pp3_outputs_to_host", "pp3_host_device_ptr", "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
                  "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy", "pp3_rollout_policy",
                  "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
                  "pp3_comm_allreduce", "pp3_comm_barrier", "pp3_render"):
@@ -128,7 +130,7 @@ EXPORTED_SYMBOLS = (
     "pp3_num_envs", "pp3_state_stride", "pp3_env_device", "pp3_reset", "pp3_step", "pp3_rollout", "pp3_set_dr",
     "pp3_set_pipeline_output", "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
     "pp3_copy_field_to_host_async", "pp3_host_malloc", "pp3_host_free", "pp3_memcpy_h2d_async",
-    "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_memcpy_d2d",
+    "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_outputs_to_host", "pp3_host_device_ptr", "pp3_memcpy_d2d",
     "pp3_fill_uniform", "pp3_step_timed", "pp3_rollout_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
     "pp3_rollout_policy",
@@ -151,6 +153,15 @@ class PinnedBlock:
         self.__array_interface__ = {"shape": (self.nbytes // 4,), "typestr": "<f4", "version": 3,
                                     "data": (self.ptr.value, False)}
         self._pool = pool
+        self._dev = None
+
+    def device_ptr(self) -> int:
+        """The block's device address (pp3_host_device_ptr; cached): kernels store into it directly."""
+        if self._dev is None:
+            d = C.c_void_p()
+            check(load().pp3_host_device_ptr(self.ptr, C.byref(d)))
+            self._dev = d.value
+        return self._dev
 
     @staticmethod
     def take(nbytes: int, pool: list) -> "PinnedBlock":
@@ -177,6 +188,9 @@ class _BlockRef:
         self.block = block
         self.ptr = block.ptr
         self.__array_interface__ = block.__array_interface__
+
+    def device_ptr(self) -> int:
+        return self.block.device_ptr()
 
 
 class DeviceBuffer:

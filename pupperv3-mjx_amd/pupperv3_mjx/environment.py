@@ -87,6 +87,13 @@ class State:
 _LAZY = ("pipeline_state", "metrics", "info", "_record", "_metrics_raw")
 
 
+# how the host API's per-step outputs reach the host (host API): the step launch
+# stores them into the page-locked block itself (STEP_WRITES_HOST), else a kernel after the launch
+# (OUTPUTS_BY_KERNEL, pp3_outputs_to_host) or copy-engine transfers
+STEP_WRITES_HOST = True
+OUTPUTS_BY_KERNEL = True
+
+
 def _ro(a):
     """Read-only view of a host array handed out in a State (JAX arrays are immutable)."""
     a = np.asarray(a)
@@ -522,8 +529,18 @@ class PupperV3Env:
         np.copyto(self._act_stage_arr, act.reshape(-1))
         _lib.check(self._L.pp3_memcpy_h2d_async(self._act_buf.ptr, self._act_stage.ptr, act.nbytes,
                                                  self._L.pp3_stream(self._h)))
-        self.step_device(self._act_buf.ptr.value)
-        return self._issue(single)
+        if not STEP_WRITES_HOST:
+            self.step_device(self._act_buf.ptr.value)
+            return self._issue(single)
+        # the step launch itself stores obs | reward | done into the page-locked output block (a
+        # one-step pp3_rollout whose trajectory rows are the block's device mapping): no copy after it
+        n, D = self.num_envs, self.observation_size
+        lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
+        dev = lease.device_ptr()
+        self._before_launch()
+        _lib.check(self._L.pp3_rollout(self._h, self._act_buf.ptr, 0, 1, C.c_void_p(dev + 4 * n * D),
+                                       C.c_void_p(dev + 4 * n * (D + 1)), C.c_void_p(dev), None))
+        return self._issue(single, lease)
 
     def rollout_device(self, actions_dev: int, action_stride: int, nsteps: int, reward_dev: Optional[int] = None,
                        done_dev: Optional[int] = None, obs_dev: Optional[int] = None,
@@ -622,15 +639,19 @@ class PupperV3Env:
         _lib.check(self._L.pp3_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(src_dev), out.nbytes))
         return out
 
-    def _issue(self, single: bool) -> DeviceState:
-        # obs | reward | done land in one page-locked block (async copies on the env's stream, one
-        # sync); the arrays are views of it and keep it leased until the last of them dies
+    def _issue(self, single: bool, lease=None) -> DeviceState:
+        # obs | reward | done land in one page-locked block (one sync); the arrays are views of it
+        # and keep it leased until the last of them dies.  `lease`: a block the launch already fills
         n, D = self.num_envs, self.observation_size
-        lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
-        base = lease.ptr.value
-        for f, off, nb in ((_abi.F_OBS, 0, 4 * n * D), (_abi.F_REWARD, 4 * n * D, 4 * n),
-                           (_abi.F_DONE, 4 * n * (D + 1), 4 * n)):
-            _lib.check(self._L.pp3_copy_field_to_host_async(self._h, f, C.c_void_p(base + off), nb))
+        if lease is None:
+            lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
+            base = lease.ptr.value
+            if OUTPUTS_BY_KERNEL:  # one kernel storing through the block's device mapping (pp3_outputs_to_host)
+                _lib.check(self._L.pp3_outputs_to_host(self._h, C.c_void_p(base)))
+            else:  # three copy-engine transfers
+                for f, off, nb in ((_abi.F_OBS, 0, 4 * n * D), (_abi.F_REWARD, 4 * n * D, 4 * n),
+                                   (_abi.F_DONE, 4 * n * (D + 1), 4 * n)):
+                    _lib.check(self._L.pp3_copy_field_to_host_async(self._h, f, C.c_void_p(base + off), nb))
         self.synchronize()
         flat = np.asarray(lease)
         obs = _ro(flat[:n * D].reshape(n, D))

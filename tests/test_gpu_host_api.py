@@ -125,3 +125,34 @@ def dict_roundtrip(w, st):
     st.info = info
     assert not w.env.holds(st)
     return st
+
+
+@pytest.mark.parametrize("mode", ["fused", "kernel", "copy"])
+def test_output_paths_return_the_device_outputs(require_gpu, mode):
+    """env.step's obs / reward / done reach the host three ways: stored by the step launch itself
+    into the page-locked block (a one-step pp3_rollout whose trajectory rows are the block's device
+    mapping, the default), by pp3_outputs_to_host after the launch, or by copy-engine transfers.
+    Each must return exactly the env's device buffers, with auto-reset and action_repeat too (the
+    trajectory rows are written at the last repeat; a done env's rows are its reset obs)."""
+    from pupperv3_mjx import environment, wrappers
+    saved = environment.STEP_WRITES_HOST, environment.OUTPUTS_BY_KERNEL
+    environment.STEP_WRITES_HOST, environment.OUTPUTS_BY_KERNEL = mode == "fused", mode != "copy"
+    try:
+        for wrapped in (False, True):
+            N = 67
+            env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=N)
+            try:
+                api = wrappers.wrap(env, episode_length=4, action_repeat=2) if wrapped else env
+                st = api.reset(make_keys(2, N))
+                rs = np.random.RandomState(5)
+                for _ in range(6):
+                    st = api.step(st, rs.uniform(-1, 1, size=(N, 12)).astype(np.float32))
+                    np.testing.assert_array_equal(st.obs, env._get(_abi.F_OBS))
+                    np.testing.assert_array_equal(st.reward, env._get(_abi.F_REWARD)[:, 0])
+                    np.testing.assert_array_equal(st.done, env._get(_abi.F_DONE)[:, 0])
+                if wrapped:  # truncation at 4 steps: every env went through an auto-reset
+                    assert np.all(st.info["steps"] <= 4)
+            finally:
+                env.close()
+    finally:
+        environment.STEP_WRITES_HOST, environment.OUTPUTS_BY_KERNEL = saved

@@ -85,7 +85,7 @@ def _bench(env, *extra, timeout=240):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_bench_launches_ranks_and_checks_the_gather(loopback_env, world):
     """`python bench.py --gpus N` as the driver runs it, without a launcher: the parent starts N
     rank processes, they join one communicator, time with barrier + max over ranks, and finish
