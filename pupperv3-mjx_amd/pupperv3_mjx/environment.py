@@ -92,6 +92,8 @@ _LAZY = ("pipeline_state", "metrics", "info", "_record", "_metrics_raw")
 # (OUTPUTS_BY_KERNEL, pp3_outputs_to_host) or copy-engine transfers
 STEP_WRITES_HOST = True
 OUTPUTS_BY_KERNEL = True
+# rollout(): trajectories up to this size are stored by the launch into page-locked host memory
+TRAJ_PINNED_MAX_BYTES = 256 << 20
 
 
 def _ro(a):
@@ -338,6 +340,7 @@ class PupperV3Env:
         self._issued = None
         self._snap_pool = []
         self._pin_pool = []    # page-locked output blocks (obs | reward | done) of issued states
+        self._traj_pool = {}   # page-locked rollout trajectory blocks, per unroll length
         self._act_stage = _lib.PinnedBlock(self.num_envs * _abi.NU * 4)  # page-locked action staging
         self._act_stage_arr = np.asarray(self._act_stage)
         self._lazy_extra = {}  # field id -> info hook (wrappers.AutoResetEpisodeEnv: the episode record)
@@ -569,14 +572,28 @@ class PupperV3Env:
             self._write_state(state)
         bufs = self._rollout_buffers(K)
         bufs[0].upload(act)
-        self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, bufs[1].ptr.value, bufs[2].ptr.value,
-                            bufs[3].ptr.value)
-        self.synchronize()
-        rew = np.empty((K, n), np.float32)
-        done = np.empty((K, n), np.float32)
-        obs = np.empty((K, n, D), np.float32)
-        for b, a in zip(bufs[1:], (rew, done, obs)):
-            b.download(a)
+        nbytes = 4 * K * n * (D + 2)
+        if nbytes <= TRAJ_PINNED_MAX_BYTES:
+            # the trajectory lands in one page-locked block that the fused launch stores into through
+            # its device mapping (no copy after the launch; the arrays are views that keep it leased)
+            lease = _lib.PinnedBlock.take(nbytes, self._traj_pool.setdefault(K, []))
+            dev = lease.device_ptr()
+            self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, dev + 4 * K * n * D, dev + 4 * K * n * (D + 1),
+                                dev)
+            self.synchronize()
+            flat = np.asarray(lease)
+            obs = _ro(flat[:K * n * D].reshape(K, n, D))
+            rew = _ro(flat[K * n * D:K * n * (D + 1)].reshape(K, n))
+            done = _ro(flat[K * n * (D + 1):].reshape(K, n))
+        else:  # a long unroll: device buffers, copied out after the launch
+            self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, bufs[1].ptr.value, bufs[2].ptr.value,
+                                bufs[3].ptr.value)
+            self.synchronize()
+            rew = np.empty((K, n), np.float32)
+            done = np.empty((K, n), np.float32)
+            obs = np.empty((K, n, D), np.float32)
+            for b, a in zip(bufs[1:], (rew, done, obs)):
+                b.download(a)
         traj = {"obs": obs, "reward": rew, "done": done}
         if single:
             traj = {k: v[:, 0] for k, v in traj.items()}

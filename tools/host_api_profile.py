@@ -64,3 +64,10 @@ for i in range(N):
     st = env.step(st, acts[i])
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+K = 30
+ra = np.random.RandomState(4).uniform(-1, 1, size=(K, E, 12)).astype(np.float32)
+for rep in range(3):
+    t = time.perf_counter()
+    st, tr = env.rollout(st, ra)
+    dt = time.perf_counter() - t
+    print(f"env.rollout(K={K}): {dt / K * 1e6:.1f} us/step = {E * K / dt / 1e6:.2f} M env-steps/s")
