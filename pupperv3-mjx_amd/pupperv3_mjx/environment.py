@@ -572,19 +572,14 @@ class PupperV3Env:
             self._write_state(state)
         bufs = self._rollout_buffers(K)
         bufs[0].upload(act)
-        nbytes = 4 * K * n * (D + 2)
-        if nbytes <= TRAJ_PINNED_MAX_BYTES:
+        blk = self._traj_block(K)
+        if blk is not None:
             # the trajectory lands in one page-locked block that the fused launch stores into through
             # its device mapping (no copy after the launch; the arrays are views that keep it leased)
-            lease = _lib.PinnedBlock.take(nbytes, self._traj_pool.setdefault(K, []))
-            dev = lease.device_ptr()
-            self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, dev + 4 * K * n * D, dev + 4 * K * n * (D + 1),
-                                dev)
+            lease, (p_obs, p_rew, p_done) = blk
+            self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, p_rew, p_done, p_obs)
             self.synchronize()
-            flat = np.asarray(lease)
-            obs = _ro(flat[:K * n * D].reshape(K, n, D))
-            rew = _ro(flat[K * n * D:K * n * (D + 1)].reshape(K, n))
-            done = _ro(flat[K * n * (D + 1):].reshape(K, n))
+            obs, rew, done = self._traj_views(lease, K)
         else:  # a long unroll: device buffers, copied out after the launch
             self.rollout_device(bufs[0].ptr.value, n * _abi.NU, K, bufs[1].ptr.value, bufs[2].ptr.value,
                                 bufs[3].ptr.value)
@@ -613,16 +608,41 @@ class PupperV3Env:
             self._write_state(state)
         bufs = self._rollout_buffers(K)
         self._before_launch()
-        _lib.check(self._L.pp3_rollout_policy(self._h, policy._h, K, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr,
-                                              bufs[3].ptr, None))
+        blk = self._traj_block(K)  # obs / reward / done straight into page-locked memory (see rollout)
+        outs = blk[1] if blk is not None else (bufs[3].ptr.value, bufs[1].ptr.value, bufs[2].ptr.value)
+        _lib.check(self._L.pp3_rollout_policy(self._h, policy._h, K, bufs[0].ptr, C.c_void_p(outs[1]),
+                                              C.c_void_p(outs[2]), C.c_void_p(outs[0]), None))
         self.synchronize()
-        traj = {"obs": np.empty((K, n, D), np.float32), "action": np.empty((K, n, _abi.NU), np.float32),
-                "reward": np.empty((K, n), np.float32), "done": np.empty((K, n), np.float32)}
-        for b, k in zip(bufs, ("action", "reward", "done", "obs")):
-            b.download(traj[k])
+        traj = {"action": np.empty((K, n, _abi.NU), np.float32)}  # (the actions stay on the device for the steps)
+        bufs[0].download(traj["action"])
+        if blk is not None:
+            traj["obs"], traj["reward"], traj["done"] = self._traj_views(blk[0], K)
+        else:
+            traj.update(obs=np.empty((K, n, D), np.float32), reward=np.empty((K, n), np.float32),
+                        done=np.empty((K, n), np.float32))
+            for b, k in zip(bufs[1:], ("reward", "done", "obs")):
+                b.download(traj[k])
         if single:
             traj = {k: v[:, 0] for k, v in traj.items()}
         return self._issue(single), traj
+
+    def _traj_block(self, K: int):
+        """A page-locked block for a K-step trajectory [obs K x N x 36H | reward K x N | done K x N] and
+        the device addresses of its three parts, or None above TRAJ_PINNED_MAX_BYTES."""
+        n, D = self.num_envs, self.observation_size
+        nbytes = 4 * K * n * (D + 2)
+        if nbytes > TRAJ_PINNED_MAX_BYTES:
+            return None
+        lease = _lib.PinnedBlock.take(nbytes, self._traj_pool.setdefault(K, []))
+        dev = lease.device_ptr()
+        return lease, (dev, dev + 4 * K * n * D, dev + 4 * K * n * (D + 1))
+
+    def _traj_views(self, lease, K: int):
+        """(obs, reward, done) read-only views of a filled _traj_block."""
+        n, D = self.num_envs, self.observation_size
+        flat = np.asarray(lease)
+        return (_ro(flat[:K * n * D].reshape(K, n, D)), _ro(flat[K * n * D:K * n * (D + 1)].reshape(K, n)),
+                _ro(flat[K * n * (D + 1):].reshape(K, n)))
 
     def _rollout_buffers(self, K: int) -> list:
         """Device buffers of rollout(): actions, reward, done, obs for K steps (kept and grown)."""

@@ -71,3 +71,19 @@ for rep in range(3):
     st, tr = env.rollout(st, ra)
     dt = time.perf_counter() - t
     print(f"env.rollout(K={K}): {dt / K * 1e6:.1f} us/step = {E * K / dt / 1e6:.2f} M env-steps/s")
+from collections import OrderedDict  # noqa: E402
+from types import SimpleNamespace  # noqa: E402
+
+from pupperv3_mjx import export  # noqa: E402
+rs = np.random.RandomState(7)
+sizes = [env.observation_size, 256, 128, 128, 24]
+layers = OrderedDict((f"hidden_{i}", {"kernel": rs.normal(scale=1 / np.sqrt(sizes[i]), size=(sizes[i], sizes[i + 1])),
+                                      "bias": np.zeros(sizes[i + 1])}) for i in range(len(sizes) - 1))
+pol = export.DevicePolicy(export.convert_params((SimpleNamespace(mean=np.zeros(sizes[0]), std=np.ones(sizes[0])),
+                                                 {"params": layers}), "elu", 0.75, 5.0, 0.25, np.zeros(12), np.ones(12),
+                                                -np.ones(12), True, 2, 30.0, 30.0), env.device)
+for rep in range(3):
+    t = time.perf_counter()
+    st, tr = env.rollout_policy(st, pol, K)
+    dt = time.perf_counter() - t
+    print(f"env.rollout_policy(K={K}): {dt / K * 1e6:.1f} us/step = {E * K / dt / 1e6:.2f} M env-steps/s")
