@@ -20,7 +20,10 @@
  * (mujoco/mujoco_mjx are absent from this container and from the GPU box, and the
  * reference's tests pin no physics values).  The RNG is pinned by the
  * Random123 threefry known-answer vectors, the latency buffers by test_utils.py:54-105,
- * the IMU lag by test_environment.py:136-156 (see tests/).
+ * the IMU lag by test_environment.py:136-156 (see tests/).  The physics shared with the
+ * kernel is pinned by known answers derived from MuJoCo's documented model without either
+ * restatement: M, invweight0, frictionloss, joint limits, resting contacts
+ * (tests/test_physics_kat.py) and pyramidal friction with impratio (tests/test_friction_kat.py).
  *
  * This file is algorithm-for-algorithm "textbook" MuJoCo over general tree arrays
  * (dense nv x nv matrices, loops over bodies/dofs/rows); the HIP kernel is an

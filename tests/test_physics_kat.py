@@ -20,10 +20,11 @@ the answers come from mechanics and from MuJoCo's documented constraint model):
   = the summed normal force at rest) and every foot penetrates by the documented equilibrium depth
   sign (r < 0, |r| below the solimp width where the impedance saturates).
 
-What stays unpinned: the pyramidal contact regulariser (R of the edge rows and its impratio
-scaling) and the friction behaviour it produces under one Newton iteration -- MuJoCo's numbers for
-it live in its C source only, which is not available here (a tilted-plane stick/slip probe of the
-oracle gave no clean analytic threshold to pin: the legged body tips and creeps first).
+Pyramidal contact friction with impratio (the edge rows' regulariser and the one-Newton-iteration
+response) is pinned in tests/test_friction_kat.py on a body that cannot tip (a solid ball on a
+slope: the exact soft-pyramid minimiser, rolling at 5/7 g sin, the Coulomb bound, impratio creep),
+and on the kernel by tests/test_gpu_kat.py.  What stays unpinned is MuJoCo's own implementation
+(both restatements are checked against its documented constraint model, not its C source).
 """
 import numpy as np
 import pytest
