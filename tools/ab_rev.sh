@@ -5,7 +5,7 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 REV=$1; NAME=${2:-$1}
 T=$(mktemp -d)
 mkdir -p $T/csrc $T/include
-for f in pp3_env.hip pp3_policy.hip pp3_comm.hip pp3_render.hip pp3_device.h; do git -C $ROOT show $REV:pupperv3-mjx_amd/csrc/$f > $T/csrc/$f 2>/dev/null || rm -f $T/csrc/$f; done
+for f in pp3_env.hip pp3_policy.hip pp3_comm.hip pp3_render.hip pp3_device.h pp3_diag.h; do git -C $ROOT show $REV:pupperv3-mjx_amd/csrc/$f > $T/csrc/$f 2>/dev/null || rm -f $T/csrc/$f; done
 git -C $ROOT show $REV:include/pupper_hip.h > $T/include/pupper_hip.h
 mkdir -p $ROOT/ab
 cd $T/csrc && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I../include -Wall -Wno-unused-result \
