@@ -19,7 +19,7 @@ def _clean_env(**extra):
     return env
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])  # 8: the driver's SCALE run on a full node
 def test_gpus_n_starts_n_distinct_ranks(n):
     out = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dry-launch"], env=_clean_env(),
                          capture_output=True, text=True, timeout=120)
