@@ -23,7 +23,8 @@
  * the IMU lag by test_environment.py:136-156 (see tests/).  The physics shared with the
  * kernel is pinned by known answers derived from MuJoCo's documented model without either
  * restatement: M, invweight0, frictionloss, joint limits, resting contacts
- * (tests/test_physics_kat.py) and pyramidal friction with impratio (tests/test_friction_kat.py).
+ * (tests/test_physics_kat.py), pyramidal friction with impratio (tests/test_friction_kat.py) and
+ * the narrow phase's distances, contact sets and sphere-box normals (tests/test_collision_kat.py).
  *
  * This file is algorithm-for-algorithm "textbook" MuJoCo over general tree arrays
  * (dense nv x nv matrices, loops over bodies/dofs/rows); the HIP kernel is an

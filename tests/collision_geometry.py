@@ -79,3 +79,61 @@ def check_record(m, pipe, cap, tol):
     assert np.all(err <= tol), (err.max(), tol)
     nbox = sum(1 for p in got if int(m.cgeom_type[pairs[p][1]]) == _abi.GEOM_BOX)
     return n, nbox, float(err.max()) if n else 0.0
+
+
+# ------------------------------------------------------------------ contact normal known answer
+# A solid ball pressed into a box by a gravity vector along the outward normal u of the box region
+# it touches (face: the face normal; edge: the bisector; corner: the diagonal), from rest.  The
+# contact problem is then symmetric under the reflections t1 -> -t1 and t2 -> -t2 of the contact
+# frame (the pyramid edges J_n +- mu J_t swap in pairs, a0 = g has no tangential part, the ball's
+# inertia is isotropic), so the exact minimiser and every Newton iterate of it have linear
+# acceleration parallel to u and zero angular acceleration, and the contact pushes back (a.u > -g).
+# A wrong normal (a face normal in the edge region, a box rotation applied the wrong way) gives a
+# tangential or angular component.
+BALL_R, BALL_M = 0.05, 1.0
+REGIONS = {"face": (1.0, 0.0, 0.0), "edge": (1.0, 0.0, 1.0), "corner": (1.0, 1.0, 1.0)}
+
+
+def ball_box_model(path, region, pen=1e-3):
+    """(model struct, qpos) of the ball touching the first box geom of the model at `path` in
+    `region`, penetrating by `pen`; gravity along -u.  Returns (struct, qpos[19], u_world)."""
+    import math
+    cm = mjcf.load(path)
+    m = cm.struct
+    m.timestep = 0.004
+    for b in range(2, _abi.NBODY):
+        m.body_mass[b] = 1e-9
+        for k in range(3):
+            m.body_inertia[b][k] = 1e-13
+    m.body_mass[1] = BALL_M
+    m.body_inertia[1][:] = [0.4 * BALL_M * BALL_R ** 2] * 3
+    m.body_ipos[1][:] = [0.0, 0.0, 0.0]
+    m.body_iquat[1][:] = [1.0, 0.0, 0.0, 0.0]
+    box = next(g for g in range(m.ncgeom) if m.cgeom_type[g] == _abi.GEOM_BOX)
+    ball = next(g for g in range(m.ncgeom) if m.cgeom_bodyid[g] != 0 and m.cgeom_type[g] == _abi.GEOM_SPHERE)
+    m.cgeom_bodyid[ball] = 1
+    m.cgeom_pos[ball][:] = [0.0, 0.0, 0.0]
+    m.cgeom_size[ball][0] = BALL_R
+    m.npair = 1
+    m.pair_g1[0], m.pair_g2[0] = ball, box
+    h = np.array(m.cgeom_size[box][:])
+    d = np.array(REGIONS[region])
+    u_loc = d / np.linalg.norm(d)
+    closest = h * d  # the face centre line / edge / corner point on the box surface
+    Rb = mjcf.quat_to_mat(np.array(m.cgeom_quat[box][:]))
+    u = Rb @ u_loc
+    centre = np.array(m.cgeom_pos[box][:]) + Rb @ (closest + u_loc * (BALL_R - pen))
+    m.gravity[:] = list(-9.81 * u)
+    mjcf.recompute_constants(cm)
+    q = np.zeros(19)
+    q[0:3], q[3] = centre, 1.0
+    q[7:] = [0.26, 0.0, -0.52, -0.26, 0.0, 0.52] * 2  # the legs (1e-9 kg) at the default pose
+    assert math.isclose(np.linalg.norm(u), 1.0)
+    return m, q, u
+
+
+def normal_residuals(qacc, u):
+    """(tangential part of the linear acceleration, |angular acceleration|, a.u) in m/s^2, rad/s^2."""
+    a, w = np.asarray(qacc[0:3]), np.asarray(qacc[3:6])
+    an = float(a @ u)
+    return float(np.linalg.norm(a - an * u)), float(np.linalg.norm(w)), an

@@ -70,3 +70,16 @@ def test_sphere_box_regions():
                     ((2, 3, 4), np.sqrt(3.0) - 0.1), ((0.9, 0, 0), -0.1 - 0.1), ((0, 0, -2.5), -0.5 - 0.1)]:
         M.cgeom_pos = [list(c), [0, 0, 0]]
         assert CG.pair_distance(M, pipe, 0, 1) == pytest.approx(want, abs=1e-12)
+
+
+@pytest.mark.parametrize("region", sorted(CG.REGIONS))
+def test_sphere_box_normal_by_region(tmp_path, region):
+    """The contact normal of each sphere-box region (collision_geometry.ball_box_model): one oracle
+    substep from rest accelerates the ball along the region's outward normal only."""
+    m, q, u = CG.ball_box_model(common.write_model(tmp_path, 1), region)
+    out = O.mj_forward(m, q, np.zeros(18), np.zeros(18), np.zeros(12))
+    assert int(out["pipe"][_abi.P_NCON]) == 1 and out["nefc"] == 12 + 4  # hinge frictionloss + 4 edges
+    tang, ang, an = CG.normal_residuals(out["qacc"], u)
+    # (the 1e-9 kg legs and their frictionloss rows leave ~1e-8 / 1e-5; a wrong normal gives O(g), O(g / r))
+    assert tang <= 1e-5 and ang <= 1e-3, (tang, ang)
+    assert an > -9.81 + 1.0, an  # the contact pushes back

@@ -59,3 +59,23 @@ def test_kernel_leg_leg_sphere_pairs_equal_closed_form(box_path):
             CG.check_record(m, pipes[i], 8, tol=TOL)
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("region", sorted(CG.REGIONS))
+def test_kernel_sphere_box_normal_by_region(tmp_path, require_gpu, region):
+    """The kernel's sphere-box normal per region (collision_geometry.ball_box_model): one substep
+    from rest accelerates the ball along the region's outward normal only (fp32: tangential
+    <= 1e-3 m/s^2 = 1e-4 g, angular <= 0.05 rad/s^2; a wrong normal gives O(g), O(g / r))."""
+    path = common.write_model(tmp_path, 1)
+    m, q, u = CG.ball_box_model(path, region)
+    e = G.env_with_model(path, m, 2)
+    try:
+        qpos = np.tile(q, (2, 1))
+        _, _, qacc, pipes = G.gpu_physics(e, qpos, np.zeros((2, 18)), np.zeros((2, 18)), np.zeros((2, 12)), 1)
+        assert int(pipes[0][_abi.P_NCON]) == 1
+        tang, ang, an = CG.normal_residuals(qacc[0], u)
+        print(f"normal KAT {region}: tangential {tang:.2e} m/s^2, angular {ang:.2e} rad/s^2, a.u {an:.4f}")
+        assert tang <= 1e-3 and ang <= 5e-2, (tang, ang)
+        assert an > -9.81 + 1.0, an
+    finally:
+        e.close()
