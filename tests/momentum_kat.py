@@ -77,3 +77,33 @@ def momentum_rates(m, q, v, qacc, h=1e-5):
     (P1, L1), (P0, L0) = at(h, qacc), at(-h, qacc)
     (_, L1z), (_, L0z) = at(h, 0 * qacc), at(-h, 0 * qacc)
     return (P1 - P0) / (2 * h), (L1 - L0) / (2 * h), (L1z - L0z) / (2 * h)
+
+
+def dr_rows(n, seed):
+    """n domain-randomisation rows: domain_randomization.domain_randomize (the reference's ranges)
+    on the nominal PD model's System, built as PupperV3Env builds `env.sys`."""
+    from pupperv3_mjx import domain_randomization as dr, rng
+    cm = common.pd_model()
+    m = cm.struct
+    nominal = dr.System(
+        geom_friction=cm.geom_friction.copy(),
+        actuator_gainprm=np.pad(np.array(m.actuator_gainprm[:], dtype=np.float64), ((0, 0), (0, 7))),
+        actuator_biasprm=np.pad(np.array(m.actuator_biasprm[:], dtype=np.float64), ((0, 0), (0, 7))),
+        body_ipos=np.array(m.body_ipos[:], dtype=np.float64),
+        body_inertia=np.array(m.body_inertia[:], dtype=np.float64),
+        body_mass=np.array(m.body_mass[:], dtype=np.float64))
+    out, _ = dr.domain_randomize(nominal, rng.split(rng.PRNGKey(seed), n))
+    return out
+
+
+def dr_edited(m, row):
+    """A copy of model struct m with one DR row written into the reference's fields
+    (domain_randomization.py: body_mass, body_inertia, body_ipos[1]; sys.tree_replace)."""
+    e = type(m).from_buffer_copy(m)
+    for b in range(_abi.NBODY):
+        e.body_mass[b] = float(row[_abi.DR_MASS + b])
+        for k in range(3):
+            e.body_inertia[b][k] = float(row[_abi.DR_INERTIA + 3 * b + k])
+    for k in range(3):
+        e.body_ipos[1][k] = float(row[_abi.DR_BASE_IPOS + k])
+    return e

@@ -18,3 +18,23 @@ def test_flight_conserves_angular_momentum_and_falls_at_g():
         # the velocity-product terms qacc must cancel are O(|dL0|): a wrong term leaves O(1) of it
         assert np.linalg.norm(dL0) > 1e-3
         assert np.linalg.norm(dL) <= 1e-6 * np.linalg.norm(dL0) + 1e-9, (dL, dL0)
+
+
+def test_domain_randomised_flight_uses_the_rows_fields():
+    """With a DR row (domain_randomization.py semantics: body_mass, body_inertia, body_ipos[1],
+    Kp / Kd) the step's dynamics are those of the model with the row written into those fields:
+    momentum computed on the edited model is conserved / falls at g, and the PD torque uses the
+    row's Kp and Kd."""
+    import test_actuator_kat as A
+    from pupperv3_mjx import _abi
+    m = K.flight_model()
+    table = K.dr_rows(6, seed=5).dr_table().astype(np.float64)
+    for i, (q, v, ctrl) in enumerate(K.flight_states(6, seed=3)):
+        _, _, qacc, pipe, _ = O.mj_step(m, q, v, np.zeros(18), ctrl, nsteps=1, dr=table[i])
+        me = K.dr_edited(m, table[i])
+        dP, dL, dL0 = K.momentum_rates(me, q, v, qacc)
+        np.testing.assert_allclose(dP / np.array(me.body_mass[1:]).sum(), np.array(m.gravity[:]), atol=1e-6)
+        assert np.linalg.norm(dL) <= 1e-6 * np.linalg.norm(dL0) + 1e-9, (dL, dL0)
+        kp, kd = table[i, _abi.DR_KP], table[i, _abi.DR_KD]
+        want = np.clip(kp * (ctrl - q[7:]) - kd * v[6:], -A.FMAX, A.FMAX)
+        np.testing.assert_allclose(pipe[_abi.P_QFRC_ACT + 6:_abi.P_QFRC_ACT + 18], want, atol=1e-9)
