@@ -225,12 +225,29 @@ def host_api_rates(model_path, E, device, keys, steps=30, warmup=3):
     return out
 
 
+def host_cores() -> dict:
+    """What the host offers this process: the machine's CPUs, the ones this process may run on,
+    and the OpenMP thread count the pool sets (OMP_NUM_THREADS is the GPU box's per-GPU CPU share;
+    the box's rules say to leave it)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return {"os_cpu_count": os.cpu_count(), "affinity": aff, "omp_num_threads": omp or None,
+            "threads": omp or aff}
+
+
 def cpu_baseline(model, cfg, states, obs, seconds_target=12.0):
-    """Time the oracle (C fp64 restatement of the same step, OpenMP over envs) on host cores."""
+    """Time the oracle (C fp64 restatement of the same step, OpenMP over envs) on every host core
+    this process may use (sched_getaffinity, or OMP_NUM_THREADS where the pool sets it), 64 envs
+    per thread."""
     import numpy as np
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    hc = host_cores()
+    threads = hc["threads"]
     n = min(states.shape[0], 64 * threads)
+    if n < 64 * threads:  # more cores than the GPU workload has envs: tile the states
+        reps = -(-64 * threads // states.shape[0])
+        states, obs = np.concatenate([states] * reps)[:64 * threads], np.concatenate([obs] * reps)[:64 * threads]
+        n = 64 * threads
     st = states[:n].copy()
     ob = obs[:n].copy()
     rs = np.random.RandomState(0)
@@ -243,9 +260,12 @@ def cpu_baseline(model, cfg, states, obs, seconds_target=12.0):
     t = time.time()
     st, ob, _, used = O.rollout(model, cfg, st, ob, acts, k, threads)
     dt = time.time() - t
-    return {"value": n * k / dt, "unit": "env-steps/s", "cores": int(used), "kind": "port",
+    return {"value": n * k / dt, "unit": "env-steps/s", "cores": int(used), "kind": "port", "host_cores": hc,
             "sample": f"{n} envs x {k} steps of the fp64 C oracle (pp3_oracle.c restatement of mj_step + env, "
-                      f"not MuJoCo), OpenMP {used} threads, {dt:.1f} s wall"}
+                      f"not MuJoCo), OpenMP {used} threads = "
+                      + ("OMP_NUM_THREADS (the pool's CPU share per GPU)" if hc["omp_num_threads"] else
+                         "every CPU in this process's affinity mask")
+                      + f", {dt:.1f} s wall"}
 
 
 def qpos_drift(env, nsub=1000, dr_row=None, terrain_row=None):
@@ -759,6 +779,15 @@ def main():
                                           "avg_launch_ms": round(half_s * 1e3, 4),
                                           "ratio": round(launch_s / half_s, 4),
                                           "note": "launch time at E / at E/2 envs (one wave per SIMD)"}
+        lat, vi = out["roofline"].get("latency"), out["roofline"].get("valu_issue")
+        # what binds the launch: the HBM traffic of the contract's `bound` is ~1 % of
+        # peak; the step is one wave's dependency chain (second wave per SIMD ~free, VALU issue ~1/3)
+        out["roofline"]["binding"] = {
+            "resource": "latency",
+            "valu_issue_frac": vi["frac"] if vi else None,
+            "latency_ratio": lat["ratio"] if lat else None,
+            "note": "the contract's bound field is the HBM roofline; the kernel is bound by the slowest "
+                    "wave's dependency chain (exposed LDS / memory latency), not by HBM or VALU issue"}
         if world == 1 and not args.no_extras:
             if not (args.dr or args.obstacles or args.auto_reset or args.policy or args.gather):
                 out["host_api"] = host_api_rates(model_path, E, device, keys)

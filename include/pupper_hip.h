@@ -447,9 +447,6 @@ int pp3_step_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stri
 int pp3_rollout_timed(pp3_env_t* env, const float* actions_dev, int64_t action_stride, int32_t nsteps,
                       float* reward_dev, float* done_dev, float* obs_dev, float* kernel_ms_total);
 
-/* Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-clock totals of env_step_kernel
- * summed over envs (n <= 16 slots); returns PP3_ERR_ARG in the production build. */
-int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset);
 /* Rendering (environment.py:545-547 PupperV3Env.render -> Brax PipelineEnv.render, the policy
  * videos of utils.py:214-293; not on the training path).  A z-buffer rasteriser over a triangle
  * soup built on the host by pupperv3_mjx/render.py from the model's visual geoms:
@@ -469,11 +466,6 @@ int pp3_render(int32_t device, const float* tris, const int32_t* tri_geom, int32
                int32_t width, const float* scene, uint8_t* out, void* stream);
 const char* pp3_render_last_error(void);
 
-/* Diagnostic builds only: per-wave record of the last env-step launch, 288 words per wave (lifetime
- * cycles, dense-Hessian substeps, max contacts, line-search evaluations, start and end stamps,
- * HW_ID, XCC_ID, then 19 per-phase cycle counts, contacts summed over substeps, substeps that
- * used the second constraint-row slot, s_memrealtime (100 MHz) at start and end, 1 unused; then 128 phase stamps and their 128 phase ids). */
-int pp3_wave_profile(uint32_t* host_out, int32_t n);
 
 /* ---------------------------------------------------------------------------------------
  * On-device MLP policy in the reference's deployment format (export.py:13-81 convert_params:

@@ -1,0 +1,31 @@
+/*
+ * pupper_hip_diag.h -- diagnostic entry points of libpupper_hip.so (not part of the drop-in
+ * boundary in pupper_hip.h; nothing on the env path calls them).  They read the per-phase and
+ * per-wave shader-clock records of a library built with -DPP3_PHASE_PROF (`make prof`, used by
+ * tests/diag_phases.py and tests/diag_waves_fused.py); the production library exports them only
+ * to return PP3_ERR_ARG, and a diagnostic library refuses pp3_create unless PP3_ALLOW_DIAG_BUILD
+ * is set.
+ */
+#ifndef PUPPER_HIP_DIAG_H_
+#define PUPPER_HIP_DIAG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Diagnostic build only (-DPP3_PHASE_PROF): per-phase shader-clock totals of env_step_kernel
+ * summed over envs (n <= 16 slots); returns PP3_ERR_ARG in the production build. */
+int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset);
+
+/* Diagnostic builds only: per-wave record of the last env-step launch, 288 words per wave (lifetime
+ * cycles, dense-Hessian substeps, max contacts, line-search evaluations, start and end stamps,
+ * HW_ID, XCC_ID, then 19 per-phase cycle counts, contacts summed over substeps, substeps that
+ * used the second constraint-row slot, s_memrealtime (100 MHz) at start and end, 1 unused; then 128 phase stamps and their 128 phase ids). */
+int pp3_wave_profile(uint32_t* host_out, int32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PUPPER_HIP_DIAG_H_ */

@@ -9,6 +9,8 @@
 // stray -D can never pass for the product.
 #pragma once
 
+#include "pupper_hip_diag.h"  // the C declarations of the diagnostic entry points
+
 #if defined(PP3_PHASE_PROF) || defined(PP3_DEBUG) || defined(PP3_TEST_RCCL_SONAME)
 #define PP3_DIAG_BUILD 1
 #else

@@ -131,7 +131,7 @@ EXPORTED_SYMBOLS = (
     "pp3_set_pipeline_output", "pp3_physics_step", "pp3_field", "pp3_copy_field_to_host", "pp3_copy_field_from_host", "pp3_synchronize",
     "pp3_copy_field_to_host_async", "pp3_host_malloc", "pp3_host_free", "pp3_memcpy_h2d_async",
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_outputs_to_host", "pp3_host_device_ptr", "pp3_memcpy_d2d",
-    "pp3_fill_uniform", "pp3_step_timed", "pp3_rollout_timed", "pp3_phase_profile", "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat",
+    "pp3_fill_uniform", "pp3_step_timed", "pp3_rollout_timed", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
     "pp3_rollout_policy",
     "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
@@ -139,6 +139,10 @@ EXPORTED_SYMBOLS = (
     "pp3_comm_last_error", "pp3_gather", "pp3_comm_allreduce", "pp3_comm_barrier",
     "pp3_render", "pp3_render_last_error",
 )
+
+# include/pupper_hip_diag.h: diagnostic entry points (per-phase / per-wave clocks of a -DPP3_PHASE_PROF
+# build; the product library exports them only to return PP3_ERR_ARG)
+DIAG_SYMBOLS = ("pp3_phase_profile", "pp3_wave_profile")
 
 
 class PinnedBlock:

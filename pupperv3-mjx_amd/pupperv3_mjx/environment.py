@@ -126,6 +126,14 @@ class DeviceState(State):
     def materialized(self) -> bool:
         return "info" in self.__dict__
 
+    def __setattr__(self, name, value):
+        # assigning a lazy field (pipeline_state, info, metrics, ...) of a state not yet read: fetch
+        # the issued values first, so the assignment is an edit unedited() sees and nothing
+        # downloaded later overwrites it
+        if name in _LAZY and "_env" in self.__dict__ and not self.materialized:
+            self._materialize()
+        object.__setattr__(self, name, value)
+
     def _materialize(self) -> None:
         if self.materialized:
             return
@@ -133,27 +141,46 @@ class DeviceState(State):
         src = self._snap
         if src is None and env._gen != self._gen:
             raise RuntimeError("DeviceState: the env launched again without preserving this state (internal error)")
+        if src is not None:
+            env.synchronize()  # the snapshot's d2d copies were queued on the env's stream
         fields = env._lazy_fields()
         got = {}
         for f in fields:
             got[f] = env._download(f, src.ptr.value + env._snap_offsets[f] if src is not None else None)
-        self.__dict__.update(env._unpack_lazy(self, got, self._single))
-        self.__dict__["_ids"] = _identity(self)
+        lazy = env._unpack_lazy(self, got, self._single)
+        for k, v in lazy.items():  # never over a value the caller already assigned
+            self.__dict__.setdefault(k, v)
+        self.__dict__["_ids"] = _identity(lazy["pipeline_state"], lazy["info"], self._out[0])
         if src is not None:
             env._snap_pool.append(src)
             self.__dict__["_snap"] = None
 
     def unedited(self) -> bool:
         """True when every array step() would upload is the very object this state was issued with."""
-        if tuple(self.__dict__.get(k) for k in ("obs", "reward", "done")) != self._out:
+        if any(self.__dict__.get(k) is not o for k, o in zip(("obs", "reward", "done"), self._out)):
             return False
-        return not self.materialized or _identity(self) == self._ids
+        if not self.materialized:
+            return True
+        d = self.__dict__
+        return _same(_identity(d["pipeline_state"], d["info"], d["obs"]), self._ids)
 
 
-def _identity(st) -> tuple:
-    ps, info = st.__dict__["pipeline_state"], st.__dict__["info"]
-    return (id(ps), id(ps.q), id(ps.qd), id(ps.qacc_warmstart), id(info),
-            tuple((k, id(v)) for k, v in info.items()), id(st.__dict__["obs"]))
+def _identity(ps, info, obs) -> tuple:
+    """The objects a state was issued with (strong references, compared by identity: an id() of a
+    freed object can be reused by a new one)."""
+    return (ps, ps.q, ps.qd, ps.qacc_warmstart, info, tuple(info.items()), obs)
+
+
+def _same(a: tuple, b: tuple) -> bool:
+    if len(a) != len(b):
+        return False
+    for x, y in zip(a, b):
+        if isinstance(x, tuple) and isinstance(y, tuple):
+            if len(x) != len(y) or any(kx != ky or vx is not vy for (kx, vx), (ky, vy) in zip(x, y)):
+                return False
+        elif x is not y:
+            return False
+    return True
 
 
 _DEFAULT_LOWER = [-1.220, -0.420, -2.790, -2.510, -3.140, -0.710, -1.220, -0.420, -2.790, -2.510, -3.140, -0.710]
@@ -344,6 +371,7 @@ class PupperV3Env:
         self._act_stage = _lib.PinnedBlock(self.num_envs * _abi.NU * 4)  # page-locked action staging
         self._act_stage_arr = np.asarray(self._act_stage)
         self._lazy_extra = {}  # field id -> info hook (wrappers.AutoResetEpisodeEnv: the episode record)
+        self._issue_capture = None  # () -> host data a wrapper attaches to each state when it is issued
         self._field_elems = {f: self.device_field(f)[1] for f in (_abi.F_STATE, _abi.F_METRICS, _abi.F_PIPELINE)}
         self._field_elems[_abi.F_EPISODE] = _abi.EP_STRIDE
         off, self._snap_offsets = 0, {}
@@ -442,6 +470,10 @@ class PupperV3Env:
         for b in (getattr(self, "_roll_bufs", None) or (0, []))[1]:
             b.free()
         self._roll_bufs = None
+        # free page-locked blocks go with their pools; leased ones are freed when their arrays die
+        for pool in (getattr(self, "_pin_pool", None), getattr(self, "_traj_pool", None)):
+            if pool is not None:
+                pool.clear()
 
     def __del__(self):
         try:
@@ -570,9 +602,9 @@ class PupperV3Env:
         K = act.size // (n * _abi.NU)
         if not self.holds(state):
             self._write_state(state)
-        bufs = self._rollout_buffers(K)
-        bufs[0].upload(act)
         blk = self._traj_block(K)
+        bufs = self._rollout_buffers(K, outputs=blk is None)
+        bufs[0].upload(act)
         if blk is not None:
             # the trajectory lands in one page-locked block that the fused launch stores into through
             # its device mapping (no copy after the launch; the arrays are views that keep it leased)
@@ -606,9 +638,9 @@ class PupperV3Env:
             raise ValueError("nsteps must be >= 1")
         if not self.holds(state):
             self._write_state(state)
-        bufs = self._rollout_buffers(K)
-        self._before_launch()
         blk = self._traj_block(K)  # obs / reward / done straight into page-locked memory (see rollout)
+        bufs = self._rollout_buffers(K, outputs=blk is None)
+        self._before_launch()
         outs = blk[1] if blk is not None else (bufs[3].ptr.value, bufs[1].ptr.value, bufs[2].ptr.value)
         _lib.check(self._L.pp3_rollout_policy(self._h, policy._h, K, bufs[0].ptr, C.c_void_p(outs[1]),
                                               C.c_void_p(outs[2]), C.c_void_p(outs[0]), None))
@@ -633,6 +665,8 @@ class PupperV3Env:
         nbytes = 4 * K * n * (D + 2)
         if nbytes > TRAJ_PINNED_MAX_BYTES:
             return None
+        for k in [k for k in self._traj_pool if k != K]:  # keep free blocks of the current length only
+            del self._traj_pool[k]
         lease = _lib.PinnedBlock.take(nbytes, self._traj_pool.setdefault(K, []))
         dev = lease.device_ptr()
         return lease, (dev, dev + 4 * K * n * D, dev + 4 * K * n * (D + 1))
@@ -644,16 +678,17 @@ class PupperV3Env:
         return (_ro(flat[:K * n * D].reshape(K, n, D)), _ro(flat[K * n * D:K * n * (D + 1)].reshape(K, n)),
                 _ro(flat[K * n * (D + 1):].reshape(K, n)))
 
-    def _rollout_buffers(self, K: int) -> list:
-        """Device buffers of rollout(): actions, reward, done, obs for K steps (kept and grown)."""
+    def _rollout_buffers(self, K: int, outputs: bool) -> list:
+        """Device buffers of rollout(): actions for K steps, and with `outputs` the reward, done and
+        obs trajectories (only for unrolls too long for the page-locked block); kept and grown."""
         cur = getattr(self, "_roll_bufs", None)
-        if cur is None or cur[0] < K:
+        n, D = self.num_envs, self.observation_size
+        sizes = [4 * K * n * _abi.NU] + ([4 * K * n, 4 * K * n, 4 * K * n * D] if outputs else [])
+        if cur is None or len(cur[1]) < len(sizes) or any(b.nbytes < s for b, s in zip(cur[1], sizes)):
             if cur is not None:
                 for b in cur[1]:
                     b.free()
-            n, D = self.num_envs, self.observation_size
-            cur = (K, [_lib.DeviceBuffer(4 * K * n * _abi.NU, self.device), _lib.DeviceBuffer(4 * K * n, self.device),
-                       _lib.DeviceBuffer(4 * K * n, self.device), _lib.DeviceBuffer(4 * K * n * D, self.device)])
+            cur = (K, [_lib.DeviceBuffer(sz, self.device) for sz in sizes])
             self._roll_bufs = cur
         return cur[1]
 
@@ -697,6 +732,7 @@ class PupperV3Env:
         if single:
             obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
         st = DeviceState(self, self._gen, single, obs, rew, done)
+        st.__dict__["_capture"] = self._issue_capture() if self._issue_capture is not None else None
         self._issued = weakref.ref(st)
         return st
 

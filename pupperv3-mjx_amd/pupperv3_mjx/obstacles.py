@@ -3,7 +3,7 @@
 Behavioural mirror of obstacles.py:16-57: the stdlib Mersenne-Twister ``random`` module is
 seeded once with ``seed`` and, per box, draws x, y and a yaw in that order, so a given seed
 produces the same boxes (pinned against a fixture generated from the reference module in
-tests/golden/obstacles_seed0.json).  Boxes are static world geoms shared by all envs; the
+tests/golden/obstacles_golden.json, made by tests/golden/make_golden.py).  Boxes are static world geoms shared by all envs; the
 HIP kernel collides every robot sphere against each of them (sphere-box narrow phase).
 """
 from __future__ import annotations

@@ -45,6 +45,7 @@ class AutoResetEpisodeEnv:
         _lib.check(env._L.pp3_set_auto_reset(env._h, self.episode_length))
         _lib.check(env._L.pp3_set_action_repeat(env._h, self.action_repeat))
         env._lazy_extra = {_abi.F_EPISODE: self._extra_info}  # info entries of the env's DeviceStates
+        env._issue_capture = lambda: (self._first_ps, self._first_obs)  # each state keeps its own
         self._first_ps, self._first_obs = None, None
 
     # brax Env surface
@@ -67,16 +68,18 @@ class AutoResetEpisodeEnv:
     def _extra_info(self, st, got, single: bool) -> dict:
         """The wrapper's info entries of a DeviceState, built when its lazy part is downloaded: the
         episode record rides along as one more lazy field (snapshotted with the rest); the first
-        state / obs change only at reset and are cached on the host then."""
+        state / obs change only at reset: cached on the host then, and captured by each state when
+        it is issued (st._capture), so a state read after a later reset still reports its own."""
         ep = got[_abi.F_EPISODE]
+        first_ps, first_obs = st.__dict__.get("_capture") or (None, None)
         sq = (lambda v: v[0]) if single else (lambda v: v)
         return {"steps": sq(ep[:, _abi.EP_STEPS].copy()),
                 "truncation": sq(ep[:, _abi.EP_TRUNCATION].copy()),
                 "episode_metrics": {"sum_reward": sq(ep[:, _abi.EP_SUM_REWARD].copy()),
                                     "length": sq(ep[:, _abi.EP_LENGTH].copy())},
                 "episode_done": np.array(st.done, dtype=np.float32),
-                "first_pipeline_state": self._first_ps,
-                "first_obs": self._first_obs}
+                "first_pipeline_state": None if first_ps is None else dict(first_ps),
+                "first_obs": first_obs}
 
     def reset(self, rng) -> State:
         st = self.env.reset(rng)
@@ -86,6 +89,7 @@ class AutoResetEpisodeEnv:
         self._first_ps = {"q": sq(first[:, 0:19].copy()), "qd": sq(first[:, 19:37].copy()),
                           "qacc_warmstart": sq(first[:, 37:55].copy())}
         self._first_obs = sq(fobs.copy())
+        st.__dict__["_capture"] = (self._first_ps, self._first_obs)  # (issued before they were read)
         return st
 
     def step(self, state: State, action) -> State:

@@ -7,16 +7,30 @@ import pytest
 
 from pupperv3_mjx import _abi, _lib
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "pupper_hip.h")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADER = os.path.join(INCLUDE, "pupper_hip.h")
+DIAG_HEADER = os.path.join(INCLUDE, "pupper_hip_diag.h")
 
 
-def _declared():
-    src = open(HEADER).read()
+def _declared(path=HEADER):
+    src = open(path).read()
     return sorted(set(re.findall(r"\b(pp3_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_what_python_binds():
     assert set(_declared()) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_diagnostic_entry_points_live_in_their_own_header():
+    """The per-phase / per-wave profilers are not part of the drop-in boundary: declared in
+    pupper_hip_diag.h only, exported by the library (refusing to run in the product build)."""
+    assert set(_declared(DIAG_HEADER)) == set(_lib.DIAG_SYMBOLS)
+    assert not set(_lib.DIAG_SYMBOLS) & set(_declared())
+    L = _lib.load()
+    for name in _lib.DIAG_SYMBOLS:
+        assert hasattr(L, name), name
+    buf = (C.c_uint64 * 16)()
+    assert L.pp3_phase_profile(buf, 16, 0) != 0  # the product build has no profiler
 
 
 def test_library_loads_and_exports_all_symbols():

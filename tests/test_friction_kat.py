@@ -41,9 +41,12 @@ R_BALL, M_BALL = 0.05, 1.0
 DP = np.array(common.DEFAULT_POSE)
 
 
-def ball_model(theta_deg, mu, iterations=None):
+def ball_model(theta_deg, mu, iterations=None, mixed=False):
     """The Pupper tree turned into a ball on a slope (see module docstring).  `iterations` overrides
-    the Newton iteration count (the reference's is 1, xml:57)."""
+    the Newton iteration count (the reference's is 1, xml:57).  mixed=True keeps each geom's own
+    compiled contact parameters (the ball's collision class, xml:51, against the floor's defaults,
+    xml:219), so the pair runs on the solmix-mixed solref / solimp (tests/test_contact_kat.py);
+    `mu` is then ignored."""
     cm = common.pd_model()
     m = cm.struct
     if iterations is not None:
@@ -62,11 +65,12 @@ def ball_model(theta_deg, mu, iterations=None):
     m.cgeom_bodyid[ball] = 1
     m.cgeom_pos[ball][:] = [0.0, 0.0, 0.0]
     m.cgeom_size[ball][0] = R_BALL
-    for g in (floor, ball):
-        m.cgeom_friction[g][0] = mu
-    m.cgeom_solref[ball][:] = m.cgeom_solref[floor][:]  # pair parameters = the floor's: no mixing
-    m.cgeom_solimp[ball][:] = m.cgeom_solimp[floor][:]
-    m.cgeom_solmix[ball] = m.cgeom_solmix[floor]
+    if not mixed:
+        for g in (floor, ball):
+            m.cgeom_friction[g][0] = mu
+        m.cgeom_solref[ball][:] = m.cgeom_solref[floor][:]  # pair parameters = the floor's: no mixing
+        m.cgeom_solimp[ball][:] = m.cgeom_solimp[floor][:]
+        m.cgeom_solmix[ball] = m.cgeom_solmix[floor]
     m.npair = 1
     m.pair_g1[0], m.pair_g2[0] = floor, ball
     th = math.radians(theta_deg)

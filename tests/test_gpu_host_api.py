@@ -156,3 +156,76 @@ def test_output_paths_return_the_device_outputs(require_gpu, mode):
                 env.close()
     finally:
         environment.STEP_WRITES_HOST, environment.OUTPUTS_BY_KERNEL = saved
+
+
+def test_reassigned_outputs_and_unread_fields_are_uploaded(require_gpu):
+    """Assigning a new obs / done array (N > 1) or a pipeline_state / info to a state nobody has
+    read yet is an edit: step() uploads it instead of failing or skipping it, and nothing
+    downloaded later overwrites the assignment."""
+    e = _env()
+    try:
+        uploads = _count_uploads(e)
+        st = e.reset(make_keys(5, N))
+        st.obs = np.full_like(st.obs, 0.5)            # N > 1: a tuple != of arrays used to raise here
+        st.done = np.zeros(N, np.float32)
+        out = e.step(st, np.zeros((N, 12), np.float32))
+        assert len(uploads) == 1
+        np.testing.assert_array_equal(out.obs[:, 36:72], np.full((N, 36), 0.5, np.float32))  # history frame
+        # a pipeline_state assigned before anything was read (the lazy part not downloaded)
+        fresh = e.step(out, np.zeros((N, 12), np.float32))
+        assert not fresh.materialized
+        from pupperv3_mjx.environment import PipelineState
+        q = np.zeros((N, 19), np.float32)
+        q[:, 2], q[:, 3] = 0.8, 1.0
+        q[:, 7:] = common.DEFAULT_POSE
+        fresh.pipeline_state = PipelineState(q=q, qd=np.zeros((N, 18), np.float32),
+                                             qacc_warmstart=np.zeros((N, 18), np.float32))
+        assert fresh.materialized and fresh.pipeline_state.q is q  # the download did not overwrite it
+        n0 = len(uploads)
+        up = e.step(fresh, np.zeros((N, 12), np.float32))
+        assert len(uploads) == n0 + 1
+        assert np.all(up.pipeline_state.q[:, 2] > 0.7)  # the lifted pose was stepped, not the old one
+        # info assigned before the lazy part was read: no KeyError, uploaded
+        nxt = e.step(up, np.zeros((N, 12), np.float32))
+        info = dict(nxt.info)
+        info["command"] = np.zeros((N, 3), np.float32)
+        nxt.info = info
+        after = e.step(nxt, np.zeros((N, 12), np.float32))
+        np.testing.assert_array_equal(after.info["command"], np.zeros((N, 3), np.float32))
+    finally:
+        e.close()
+
+
+def test_old_state_read_after_device_launches(require_gpu):
+    """An unread state whose env has since launched on its own stream (step_device, no host
+    synchronisation) reads its own snapshot, not the next state's data."""
+    e = _env()
+    try:
+        st = e.reset(make_keys(6, N))
+        st = e.step(st, np.zeros((N, 12), np.float32))
+        want = e._get(_abi.F_STATE).copy()
+        from pupperv3_mjx import _lib
+        buf = _lib.DeviceBuffer(N * 12 * 4, e.device)
+        buf.upload(np.random.RandomState(1).uniform(-1, 1, (N, 12)).astype(np.float32))
+        for _ in range(5):
+            e.step_device(buf.ptr.value)
+        np.testing.assert_array_equal(st._record, want)
+        buf.free()
+    finally:
+        e.close()
+
+
+def test_wrapper_states_keep_their_first_state(require_gpu):
+    """info['first_obs'] / ['first_pipeline_state'] of a wrapper state read after a later reset
+    are those of the reset the state descends from."""
+    w = wrappers.wrap(_env(), episode_length=50)
+    try:
+        s1 = w.reset(make_keys(7, N))
+        s1 = w.step(s1, np.zeros((N, 12), np.float32))
+        first1 = np.array(w._first_obs)
+        s2 = w.reset(make_keys(8, N))
+        assert np.any(np.array(w._first_obs) != first1)
+        np.testing.assert_array_equal(s1.info["first_obs"], first1)
+        np.testing.assert_array_equal(s2.info["first_obs"], w._first_obs)
+    finally:
+        w.env.close()
