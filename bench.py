@@ -569,19 +569,19 @@ def main():
             _lib.check(L.pp3_rollout_policy(env._h, policy._h, args.warmup, acts.ptr, None, None, None, None))
         else:
             _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, args.warmup, C.byref(ms)))
-    if rollout:
+    if rollout or policy is not None:
         snap = dev_snapshot()  # the timed window's start state
 
     env.synchronize()
     barrier()
     t0 = time.perf_counter()
     if policy is not None:
-        # generate_unroll with the policy in the loop: pp3_rollout_policy (per step the MLP on the
-        # obs buffer, then the env step; action / reward / done / obs trajectories written)
-        _lib.check(L.pp3_rollout_policy(env._h, policy._h, args.steps, C.c_void_p(act_at(args.warmup)),
-                                        traj[0].ptr, traj[1].ptr, traj[2].ptr, None))
-        env.synchronize()
-        kernel_ms = (time.perf_counter() - t0) * 1e3  # policy + env step per iteration (no per-kernel events)
+        # generate_unroll with the policy in the loop: pp3_rollout_policy, ONE fused launch (per
+        # step the workgroup's MLP on its envs' observations, then the env step; action / reward /
+        # done / obs trajectories written), HIP events around it
+        _lib.check(L.pp3_rollout_policy_timed(env._h, policy._h, args.steps, C.c_void_p(act_at(args.warmup)),
+                                              traj[0].ptr, traj[1].ptr, traj[2].ptr, C.byref(ms)))
+        kernel_ms = ms.value
     elif not args.gather and rollout:
         _lib.check(L.pp3_rollout_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps,
                                        traj[0].ptr, traj[1].ptr, traj[2].ptr, C.byref(ms)))
@@ -631,11 +631,50 @@ def main():
             print(f"rank {rank}: fused rollout differs from single-step launches: {per_step}", file=sys.stderr, flush=True)
         for b in traj:
             b.free()
+    if policy is not None:
+        # the same K steps again as the unfused loop (per step a pp3_policy_act launch on the obs
+        # buffer, then a single-step launch) from the kept start state: actions and end state must
+        # be bit-equal to the fused launch's
+        K = args.steps
+        end_dev = dev_snapshot()
+        a_fused = np.empty((K, E, 12), np.float32)
+        _lib.check(L.pp3_memcpy_d2h(a_fused.ctypes.data_as(C.c_void_p), C.c_void_p(act_at(args.warmup)), a_fused.nbytes))
+        dev_restore(snap)
+        rbuf = _lib.DeviceBuffer(4 * K * E * 12, device)
+        obs_ptr = env.device_field(_abi.F_OBS)[0]
+        env.synchronize()
+        tr0 = time.perf_counter()
+        for t in range(K):
+            policy.act(obs_ptr, env.observation_size, E, rbuf.ptr.value + 4 * t * E * 12, 12, stream=stream)
+            _lib.check(L.pp3_step(env._h, C.c_void_p(rbuf.ptr.value + 4 * t * E * 12), None))
+        env.synchronize()
+        unfused_ms = (time.perf_counter() - tr0) * 1e3
+        a_unf = np.empty_like(a_fused)
+        rbuf.download(a_unf)
+        rbuf.free()
+        end = {f: np.empty((E, env.device_field(f)[1]), np.float32) for f in snap_fields}
+        for f, a in end.items():
+            end_dev[f].download(a)
+        differ = [int(f) for f, v in end.items() if not np.array_equal(env._get(f).view(np.uint32), v.view(np.uint32))]
+        per_step = {"launches": 2 * K, "ms_per_step": round(unfused_ms / K, 4),
+                    "env_steps_per_s": round(E * K / (unfused_ms / 1e3), 1),
+                    "note": "the same steps as the unfused loop: per step a pp3_policy_act launch, then a pp3_step "
+                            "launch (host loop, wall clock)",
+                    "actions_bit_equal": bool(np.array_equal(a_fused.view(np.uint32), a_unf.view(np.uint32))),
+                    "bit_equal_to_rollout": not differ}
+        if differ:
+            per_step["differing_fields"] = differ
+        if differ or not per_step["actions_bit_equal"]:
+            print(f"rank {rank}: fused policy rollout differs from the unfused loop: {per_step}", file=sys.stderr, flush=True)
+        for b in list(end_dev.values()) + list(snap.values()):
+            b.free()
+        for b in traj:
+            b.free()
     # the timed window's end state (rank 0's shard; after the replay when it is bit-equal): equal
     # hashes across kernel builds mean the A/B variants ran the same trajectories, so a timing
     # difference is code speed, not a changed workload
     import hashlib
-    state_sha16 = hashlib.sha256((end[_abi.F_STATE] if rollout else env._get(_abi.F_STATE)).tobytes()).hexdigest()[:16]
+    state_sha16 = hashlib.sha256((end[_abi.F_STATE] if (rollout or policy is not None) else env._get(_abi.F_STATE)).tobytes()).hexdigest()[:16]
     gather_info = None
     if args.gather:
         # untimed: the same K steps' kernels alone (events), then the gather alone
@@ -675,9 +714,10 @@ def main():
         K = args.steps
         value = E * world * K / wall_max
         launch_s = kernel_ms_max / 1e3 / K  # kernel time per env step of the batch
-        spl = K if rollout else 1  # env steps per launch
+        fused_policy = policy is not None and (env.config_struct.ncon_max or 8) == 8
+        spl = K if (rollout or fused_policy) else 1  # env steps per launch
         bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr,
-                                             trajectory=rollout)
+                                             trajectory=rollout or policy is not None)
         achieved = bpe * E / launch_s / 1e9
         traffic, valu, epw, tsrc, flops, fsrc = None, None, 2, None, None, None
         if os.path.exists(TRAFFIC_FILE):
@@ -724,13 +764,15 @@ def main():
             "launch": (f"rollout: the {K} timed steps fused into one pp3_rollout launch (per-step reward/done/obs "
                        "trajectories written); per_step_launch = the same steps as single-step launches"
                        if rollout else
-                       ("policy: pp3_rollout_policy, per step the MLP launch on the obs buffer then the env step "
-                        "(action/reward/done/obs trajectories written), one C call for the K steps"
+                       ("policy: pp3_rollout_policy, the K steps as ONE fused launch (8-wave workgroups of 16 envs run "
+                        "the MLP before each step; action/reward/done/obs trajectories written); per_step_launch = "
+                        "the same steps as per-step policy + step launches"
                         if policy is not None else "step: one pp3_step launch per env step")),
             "per_step_launch": per_step,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "kernel": "pp3::env_step_kernel<%d, %s>" % (env.config_struct.ncon_max or 8, "true" if rollout else "false"),
+                         "kernel": ("pp3::env_step_kernel<8, true, 8> (policy MLP fused)" if fused_policy else
+                                    "pp3::env_step_kernel<%d, %s>" % (env.config_struct.ncon_max or 8, "true" if rollout else "false")),
                          "steps_per_launch": spl, "bytes_per_env_step": bpe,
                          "algorithmic_bytes_per_launch": bpe * E * spl,
                          "launch_ms": round(launch_s * spl * 1e3, 4),

@@ -488,12 +488,18 @@ int pp3_policy_out_dim(const pp3_policy_t* policy);
 int pp3_policy_destroy(pp3_policy_t* policy);
 /* The unroll of brax's generate_unroll with the policy in the loop ([ext] brax 0.12.1
  * training/acting.py: actions = policy(obs), state = env.step(state, actions), nsteps times), on the
- * env's stream with no host round trip: step t launches the policy on the env's observation buffer,
- * writing actions_dev + t * N * 12 (f32[nsteps][N][12], required: the trajectory's actions), then
- * the env step on them; reward / done / obs trajectories as pp3_rollout (optional).  The policy must
- * have 12 outputs and 36H inputs and live on the env's device. */
+ * env's stream with no host round trip: before step t the policy acts on the env's observation
+ * buffer, writing actions_dev + t * N * 12 (f32[nsteps][N][12], required: the trajectory's
+ * actions), then the env steps on them; reward / done / obs trajectories as pp3_rollout
+ * (optional).  ONE launch for the nsteps steps (workgroups of 16 envs run the policy's MLP, the
+ * code of pp3_policy_act, before each step: the actions equal pp3_policy_act's bit for bit); with
+ * max_contacts = 16 or action_repeat > 1, per step a pp3_policy_act launch then a step launch.
+ * The policy must have 12 outputs and 36H inputs and live on the env's device. */
 int pp3_rollout_policy(pp3_env_t* env, pp3_policy_t* policy, int32_t nsteps, float* actions_dev,
                        float* reward_dev, float* done_dev, float* obs_dev, void* stream);
+/* The same bracketed by HIP events on the handle's stream (kernel_ms_total = their elapsed time). */
+int pp3_rollout_policy_timed(pp3_env_t* env, pp3_policy_t* policy, int32_t nsteps, float* actions_dev,
+                             float* reward_dev, float* done_dev, float* obs_dev, float* kernel_ms_total);
 const char* pp3_policy_last_error(void);
 
 /* ---------------------------------------------------------------------------------------

@@ -29,6 +29,7 @@
 
 #include "pp3_device.h"
 #include "pp3_diag.h"
+#include "pp3_mlp.h"
 
 namespace pp3 {
 
@@ -464,7 +465,7 @@ __device__ __forceinline__ PairLoad load_pair(const DevModel& m, int p) {
   r.v[6] = *reinterpret_cast<const v4f*>(&m.pair_con[p]);
   return r;
 }
-template <int NC>
+template <int NC, int NWV = 1>
 __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, PairLoad pl, float& dist, float pos[3],
                                        float nrm[3], v4f& pc0) {
   PairRec rec;
@@ -511,7 +512,7 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, P
     if (m.terrain) {  // per-env terrain: this env's box in slot -1 - s2 (rows padded to an even env count)
       typedef float v4f __attribute__((ext_vector_type(4)));
       typedef __attribute__((address_space(1))) const v4f GF4;
-      const int env_raw = 2 * blockIdx.x + (threadIdx.x >> 5);
+      const int env_raw = 2 * NWV * blockIdx.x + (threadIdx.x >> 5);  // (NWV waves = 2 NWV envs per workgroup)
       const GF4* t = (const GF4*)(uintptr_t)m.terrain + ((size_t)env_raw * m.nbox + (-1 - rec.s2)) * 4;
       const v4f t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
       p2[0] = t0.x; p2[1] = t0.y; p2[2] = t0.z;
@@ -573,7 +574,7 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const v4f& pc0, int
 // NC pairs penetrate, the NC deepest are kept (same rule as the oracle).  Returns lane c's
 // contact support (pair_sup of contact c; 4 = no contact): the Newton phases read contact
 // supports with v_readlane from this register instead of LDS round trips per contact.
-template <int NC>
+template <int NC, int NWV = 1>
 __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h, const PairLoad& pre) {
   int nhit = 0;
   for (int base = 0; base < m.npair; base += HW) {
@@ -582,7 +583,7 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
     v4f pc0;
     // the first 32 pairs' records were fetched at the substep start (they arrive during kinematics)
     const PairLoad pl = base == 0 ? pre : load_pair(m, p < m.npair ? p : 0);
-    const bool hit = narrow(s, m, pl, dist, pos, nrm, pc0) && (p < m.npair);
+    const bool hit = narrow<NC, NWV>(s, m, pl, dist, pos, nrm, pc0) && (p < m.npair);
     const uint32_t mask = hballot(hit, h);
     const int slot = nhit + __popc(mask & ((1u << l) - 1u));
     if (hit) {
@@ -628,7 +629,7 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
       if (keep[t]) {
         float dist, pos[3], nrm[3];
         v4f pc0;
-        narrow(s, m, load_pair(m, keep_p[t]), dist, pos, nrm, pc0);
+        narrow<NC, NWV>(s, m, load_pair(m, keep_p[t]), dist, pos, nrm, pc0);
         store_contact(s, pc0, slot[t], keep_p[t], dist, pos, nrm);
       }
     }
@@ -1294,7 +1295,7 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // one physics substep (mj_step): forward + Newton + Euler.  `integrate` = false for reset
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
-template <int NC>
+template <int NC, int NWV = 1>
 __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev,
                                        const KinConst& kc PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
@@ -1326,7 +1327,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
   int lsup = 4;  // lane c: support of contact c (4 = none)
-  { lsup = collision(s, m, l, h, pair_pf); SYNC(); }
+  { lsup = collision<NC, NWV>(s, m, l, h, pair_pf); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   // the PairCon of contact c = l / 4 for the first batch of phase 13's edge rows (lane e = 4c + k),
   // loaded here unpinned: it arrives during the limit/actuation and M-entry phases
@@ -2159,10 +2160,24 @@ struct StepArgs {
   float* traj_obs;       // [nsteps][N][36H]
 };
 
-template <int NC, bool FUSED>
-__global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
-  __shared__ Shared<NC> sh[2];
-  const int nsteps = FUSED ? a_arg.nsteps : 1;
+// The fused policy rollout (pp3_rollout_policy): the env step kernel with eight waves = 16 envs
+// per workgroup, whose waves run the exported MLP on their 16 envs' observations (pp3_mlp.h
+// mlp_tile, the code of pp3_policy_act) before every step, into the step's action row.
+struct PolicyStepArgs {
+  StepArgs s;       // s.actions = act: step t reads the actions the MLP wrote at t * s.act_stride
+  float* act;       // [nsteps][N][12] action trajectory (written by the MLP)
+  pp3pol::Net net;  // the policy (device weight pointers)
+};
+
+template <int NC, bool FUSED, int NWV = 1>
+__global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
+    typename std::conditional<(NWV > 1), PolicyStepArgs, StepArgs>::type a_arg) {
+  static_assert(NWV == 1 || (FUSED && NWV == pp3pol::NWAVE), "the policy rollout is fused, one MLP tile per workgroup");
+  __shared__ Shared<NC> sh[2 * NWV];
+  static_assert(NWV == 1 || sizeof(sh) >= pp3pol::TILE_BUF_BYTES, "the MLP's LDS scratch aliases the envs' blocks");
+  int nsteps;
+  if constexpr (NWV > 1) nsteps = a_arg.s.nsteps;
+  else nsteps = FUSED ? a_arg.nsteps : 1;
   constexpr bool TG = true;  // trajectory rows (optional pointers) written by both kernels: free in the single-step one
 #ifdef PP3_PHASE_PROF
   const uint32_t t_start_ = shader_cycles();
@@ -2180,12 +2195,30 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   for (int it = 0;;) {
   const GArgs* ap = (const GArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   if (FUSED) asm volatile("" : "+s"(ap));
-  const StepArgs& a = FUSED ? *(const StepArgs*)ap : a_arg;
-  int lane = threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)
+  const StepArgs* ap_step;
+  if constexpr (NWV > 1) ap_step = (const StepArgs*)ap;
+  else ap_step = FUSED ? (const StepArgs*)ap : &a_arg;
+  const StepArgs& a = *ap_step;
+  if constexpr (NWV > 1) {
+    // policy-in-the-loop: the workgroup's MLP on its 16 envs' current observations (the previous
+    // step's, or the reset's), into this step's action row; its LDS scratch is the envs' blocks
+    // (nothing in them lives across steps).  The barrier makes every wave's previous-step stores
+    // (obs rows) visible; mlp_tile ends with one, after which the actions are visible.
+    typedef __attribute__((address_space(4))) const PolicyStepArgs GPArgs;
+    const GPArgs& pa = *(const GPArgs*)ap;
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    mlp_tile(pa.net, a.obs_out, PP3_OBS_DIM * ((const DevModel*)(const GModel*)a.m)->H,
+             pa.act + (size_t)it * a.act_stride, NU, a.N, blockIdx.x * pp3pol::TILE, *reinterpret_cast<pp3pol::TileBuf*>(sh),
+             threadIdx.x);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  int lane = NWV > 1 ? (int)(threadIdx.x & (WAVE - 1)) : (int)threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)
   if (FUSED) asm volatile("" : "+v"(lane));
+  const int wv = NWV > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;  // this wave in the workgroup
   const int h = lane >> 5, l = lane & (HW - 1);
-  Shared<NC>& s = sh[h];
-  const int env_raw = 2 * blockIdx.x + h;
+  Shared<NC>& s = sh[2 * wv + h];
+  const int env_raw = 2 * (blockIdx.x * NWV + wv) + h;
   const bool own = env_raw < a.N;
   const int env = own ? env_raw : a.N - 1;
   const DevModel& m = *(const DevModel*)(const GModel*)a.m;  // constant AS: uniform reads -> s_load
@@ -2308,7 +2341,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    const int wgt = substep(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
+    const int wgt = substep<NC, NWV>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
     heavy = wgt >= PP3_HEAVY2 ? 2 : (wgt >= PP3_HEAVY ? 1 : 0);
   }
   if (n_frames > 0) {  // the last substep's Euler step (the others ran inside the next kinematics)
@@ -2532,6 +2565,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_step_kernel(StepArgs a_arg) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
 #ifdef PP3_PHASE_PROF
+  static_assert(NWV == 1, "the per-wave profile records index waves by workgroup");
   const int lane = threadIdx.x;
   if (lane < NPROF - 1 && blockIdx.x < MAXWAVE) g_prof[blockIdx.x][lane] += pf->acc;
   if (lane == 0 && blockIdx.x < MAXWAVE) {
@@ -3305,6 +3339,13 @@ int pp3_reset(pp3_env_t* e, const uint32_t* keys_dev, const uint8_t* mask_dev, v
 // runs its envs' steps back to back, so a slow wave of step t no longer holds up the whole batch
 // at step t + 1).  With action_repeat > 1 (auto-reset mode) each wrapper step stays `repeat`
 // single-step launches.
+// tests / A-B only (PP3_POLICY_UNFUSED=1 in the environment): the policy rollout as per-step
+// policy + step launches even where the fused kernel applies
+static const bool g_policy_unfused = [] {
+  const char* v = getenv("PP3_POLICY_UNFUSED");
+  return v && v[0] == '1';
+}();
+
 static int launch_steps(pp3_env_t* e, const float* actions_dev, int64_t action_stride, int32_t nsteps,
                         float* traj_reward, float* traj_done, float* traj_obs, bool fused, void* stream) {
   HIPCHK(hipSetDevice(e->device));
@@ -3371,13 +3412,55 @@ int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float
   if (!e || !policy || !actions_dev) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: null argument");
   if (nsteps < 1) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: nsteps must be >= 1");
   if (pp3_policy_out_dim(policy) != NU) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: the policy must have 12 outputs");
+  if (pp3_policy_device(policy) != e->device) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: policy and env on different devices");
   const size_t on = (size_t)e->N * PP3_OBS_DIM * e->H;
   const hipStream_t st = stream_of(e, stream);
+  const int repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;
+#ifndef PP3_PHASE_PROF
+  if (e->nc == 8 && repeat == 1 && !g_policy_unfused) {
+    // ONE launch for the K steps: 8-wave workgroups of 16 envs run the MLP (mlp_tile, the code of
+    // pp3_policy_act) on their envs' observations before each step, then each wave steps its two
+    // envs (env_step_kernel<8, true, 8>)
+    HIPCHK(hipSetDevice(e->device));
+    PolicyStepArgs pa;
+    StepArgs& a = pa.s;
+    a.m = e->dmodel;
+    a.state = e->state;
+    a.obs_in = e->obs;
+    a.obs_out = e->obs;
+    a.actions = actions_dev;
+    a.reward = e->reward;
+    a.done = e->done;
+    a.metrics = e->metrics;
+    a.dr = e->dr_on ? e->dr : nullptr;
+    a.pipe = e->pipe_on ? e->pipe : nullptr;
+    a.episode = e->episode_length > 0 ? e->episode : nullptr;
+    a.first_state = e->first_state;
+    a.first_obs = e->first_obs;
+    a.episode_length = e->episode_length;
+    a.N = e->N;
+    a.repeat = 1;
+    a.phase = 0;
+    a.nsteps = nsteps;
+    a.act_stride = (int64_t)e->N * NU;
+    a.traj_reward = reward_dev;
+    a.traj_done = done_dev;
+    a.traj_obs = obs_dev;
+    pa.act = actions_dev;
+    pa.net = *pp3_policy_net(policy);
+    const dim3 grid((e->N + pp3pol::TILE - 1) / pp3pol::TILE), block(WAVE * pp3pol::NWAVE);
+    hipLaunchKernelGGL((env_step_kernel<8, true, pp3pol::NWAVE>), grid, block, 0, st, pa);
+    HIPCHK(hipGetLastError());
+    return PP3_OK;
+  }
+#endif
+  // per step: the policy launch on the env's obs buffer, then one single-step launch that writes
+  // this step's trajectory rows (max_contacts = 16, whose blocks do not fit 16 envs per
+  // workgroup; action_repeat > 1, whose wrapper step is `repeat` launches)
   for (int t = 0; t < nsteps; t++) {
     float* act = actions_dev + (size_t)t * e->N * NU;
     if (pp3_policy_act(policy, e->obs, PP3_OBS_DIM * e->H, e->N, act, NU, (void*)st) != PP3_OK)
       return set_err(PP3_ERR_ARG, std::string("pp3_rollout_policy: ") + pp3_policy_last_error());
-    // one single-step launch; it writes this step's trajectory rows
     const int rc = launch_steps(e, act, 0, 1, reward_dev ? reward_dev + (size_t)t * e->N : nullptr,
                                 done_dev ? done_dev + (size_t)t * e->N : nullptr, obs_dev ? obs_dev + (size_t)t * on : nullptr,
                                 false, (void*)st);
@@ -3707,6 +3790,19 @@ int pp3_rollout_timed(pp3_env_t* e, const float* actions_dev, int64_t action_str
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipEventRecord(e->ev0, e->stream));
   const int rc = pp3_rollout(e, actions_dev, action_stride, nsteps, reward_dev, done_dev, obs_dev, e->stream);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(e->ev1, e->stream));
+  HIPCHK(hipEventSynchronize(e->ev1));
+  HIPCHK(hipEventElapsedTime(kernel_ms_total, e->ev0, e->ev1));
+  return PP3_OK;
+}
+
+int pp3_rollout_policy_timed(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float* actions_dev,
+                             float* reward_dev, float* done_dev, float* obs_dev, float* kernel_ms_total) {
+  if (!e || !policy || !actions_dev || !kernel_ms_total) return set_err(PP3_ERR_ARG, "null argument");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipEventRecord(e->ev0, e->stream));
+  const int rc = pp3_rollout_policy(e, policy, nsteps, actions_dev, reward_dev, done_dev, obs_dev, e->stream);
   if (rc) return rc;
   HIPCHK(hipEventRecord(e->ev1, e->stream));
   HIPCHK(hipEventSynchronize(e->ev1));

@@ -2,16 +2,9 @@
 // (export.py:13-81 convert_params: dense layers, observation normalisation folded into the
 // first layer, final layer = the mean half of the Gaussian head, final activation tanh).
 //
-// One workgroup = 8 waves (2 per SIMD) = a tile of 16 environments; every layer is a
-// [16 x K] x [K x M] product on the f32-input matrix cores (v_mfma_f32_16x16x4_f32: exact f32
-// products, f32 accumulation), the eight waves splitting the layer's 16-column output tiles.
-// Activations stay in LDS between layers; weights are read straight from global memory (the
-// whole MLP is a few hundred KB and stays L2-resident across workgroups) in MFMA-fragment
-// order: the host stores, per 16-column tile and group of 4 k-blocks, the 64 lanes' B values
-// as one float4 per lane, so one 16-byte load per lane (1 KB contiguous per wave) feeds four
-// MFMAs -- a row-major layout would make every MFMA's B operand a 4-row gather.  32 k-blocks
-// of a tile are in flight before its MFMAs.  A: lane l holds X[row l&15][k0 + (l>>4)],
-// B: W[k0 + (l>>4)][c0 + (l&15)], C/D: col l&15, row 4(l>>4)+r.
+// One workgroup = 8 waves (2 per SIMD) = a tile of 16 environments; the tile's MLP is
+// pp3_mlp.h mlp_tile (f32 MFMA layer products, activations in LDS, weights in MFMA-fragment
+// order), the same code the fused policy rollout runs inside the env step kernel.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -19,103 +12,15 @@
 #include <string>
 #include <vector>
 
+#include "pp3_mlp.h"
 #include "pupper_hip.h"
 
 namespace pp3pol {
 
-constexpr int TILE = 16;                 // environments per workgroup
-constexpr int NWAVE = 8;
-constexpr int MAXW = PP3_POLICY_MAX_WIDTH;  // widest layer (padded)
-
-struct Layer {
-  const float* w;  // fragment order [Mp/16][ngrp][64 lanes][4], zero padded
-  const float* b;  // [Mp]
-  int K, Kp, M, Mp, act;
-  int ngrp;  // groups of 4 k-blocks (16 inputs)
-};
-struct Net {
-  Layer layer[PP3_POLICY_MAX_LAYERS];
-  int n_layers, in_dim, out_dim;
-};
-
-__device__ __forceinline__ float activate(float x, int act) {
-  switch (act) {
-    case PP3_ACT_RELU: return fmaxf(x, 0.0f);
-    case PP3_ACT_ELU: return x > 0.0f ? x : expm1f(x);
-    case PP3_ACT_TANH: return tanhf(x);
-    case PP3_ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
-    default: return x;
-  }
-}
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int CG = 8;  // groups of 4 k-blocks (32 k-blocks = 128 inputs) per chunk
-
 __global__ __launch_bounds__(64 * NWAVE) void mlp_kernel(Net net, const float* __restrict__ obs, int obs_stride,
                                                          float* __restrict__ act, int act_stride, int n) {
-  __shared__ float buf[2][TILE][MAXW + 4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row0 = blockIdx.x * TILE;
-  // observation tile -> LDS (rows past n are zero)
-  for (int i = tid; i < TILE * net.layer[0].Kp; i += 64 * NWAVE) {
-    const int r = i / net.layer[0].Kp, k = i - r * net.layer[0].Kp;
-    const int row = row0 + r;
-    buf[0][r][k] = (row < n && k < net.in_dim) ? obs[(size_t)row * obs_stride + k] : 0.0f;
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int li = 0; li < net.n_layers; li++) {
-    const Layer L = net.layer[li];
-    const float(*X)[MAXW + 4] = buf[cur];
-    float(*Y)[MAXW + 4] = buf[cur ^ 1];
-    const int ntile = L.Mp / TILE;
-    const bool last = li == net.n_layers - 1;
-    for (int t = wave; t < ntile; t += NWAVE) {
-      const int c0 = t * TILE;
-      // two independent accumulators (even / odd k blocks) cover the dependent MFMA latency
-      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
-      const int ar = lane & 15, kk = lane >> 4;
-      const int nblk = L.Kp / 4;
-      for (int g0 = 0; g0 < L.ngrp; g0 += CG) {
-        f32x4 bq[CG];
-        float av[CG][4];
-        const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
-#pragma unroll
-        for (int q = 0; q < CG; q++) {  // every load of the chunk in flight together
-          bq[q] = (g0 + q < L.ngrp) ? wf[(size_t)q * 64] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int kb = 4 * (g0 + q) + j;
-            av[q][j] = kb < nblk ? X[ar][4 * kb + kk] : 0.0f;
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < CG; q++) {
-          if (g0 + q < L.ngrp) {  // uniform; padded blocks of a ragged group multiply zeros
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][0], bq[q].x, acc, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][1], bq[q].y, acc1, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][2], bq[q].z, acc, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][3], bq[q].w, acc1, 0, 0, 0);
-          }
-        }
-      }
-      acc += acc1;
-      const int col = c0 + (lane & 15);
-      const float bias = L.b[col];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = 4 * (lane >> 4) + r;
-        const float v = activate(acc[r] + bias, L.act);
-        if (!last) {
-          Y[row][col] = v;
-        } else if (col < L.M && row0 + row < n) {
-          act[(size_t)(row0 + row) * act_stride + col] = v;
-        }
-      }
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
+  __shared__ TileBuf buf;
+  mlp_tile(net, obs, obs_stride, act, act_stride, n, blockIdx.x * TILE, buf, threadIdx.x);
 }
 
 }  // namespace pp3pol
@@ -211,6 +116,13 @@ int pp3_policy_act(pp3_policy_t* p, const float* obs_dev, int64_t obs_stride, in
 }
 
 int pp3_policy_out_dim(const pp3_policy_t* p) { return p ? p->net.out_dim : 0; }
+
+}  // extern "C"
+
+const pp3pol::Net* pp3_policy_net(const pp3_policy_t* p) { return p ? &p->net : nullptr; }
+int pp3_policy_device(const pp3_policy_t* p) { return p ? p->device : -1; }
+
+extern "C" {
 
 int pp3_policy_destroy(pp3_policy_t* p) {
   if (!p) return PP3_OK;

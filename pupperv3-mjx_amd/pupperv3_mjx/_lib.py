@@ -75,6 +75,7 @@ def load() -> C.CDLL:
     L.pp3_policy_out_dim.argtypes = [vp]
     L.pp3_policy_destroy.argtypes = [vp]
     L.pp3_rollout_policy.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+    L.pp3_rollout_policy_timed.argtypes = [vp, vp, i32, vp, vp, vp, vp, C.POINTER(C.c_float)]
     L.pp3_policy_last_error.restype = C.c_char_p
     L.pp3_stream.argtypes = [vp]
     L.pp3_stream.restype = vp
@@ -102,7 +103,7 @@ def load() -> C.CDLL:
                  "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
                  "pp3_outputs_to_host", "pp3_host_device_ptr", "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
                  "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy", "pp3_rollout_policy",
-                 "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
+                 "pp3_rollout_policy_timed", "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
                  "pp3_comm_allreduce", "pp3_comm_barrier", "pp3_render"):
         getattr(L, name).restype = C.c_int
     if L.pp3_abi_version() != _abi.ABI_VERSION:
@@ -133,7 +134,7 @@ EXPORTED_SYMBOLS = (
     "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h", "pp3_outputs_to_host", "pp3_host_device_ptr", "pp3_memcpy_d2d",
     "pp3_fill_uniform", "pp3_step_timed", "pp3_rollout_timed", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
-    "pp3_rollout_policy",
+    "pp3_rollout_policy", "pp3_rollout_policy_timed",
     "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
     "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_comm_rank", "pp3_comm_world",
     "pp3_comm_last_error", "pp3_gather", "pp3_comm_allreduce", "pp3_comm_barrier",
