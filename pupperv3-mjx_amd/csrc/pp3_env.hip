@@ -2169,6 +2169,26 @@ struct PolicyStepArgs {
   pp3pol::Net net;  // the policy (device weight pointers)
 };
 
+// The policy's MLP on this workgroup's tile, out of line (PP3_MLP_NOINLINE, the default): its
+// registers are allocated on their own instead of shaping the env step's allocation around it
+// (inlined, the fused kernel spilled 17 VGPRs; the step alone spills none).
+#ifndef PP3_MLP_PF
+#define PP3_MLP_PF 1
+#endif
+#ifndef PP3_MLP_NOINLINE
+#define PP3_MLP_NOINLINE 1
+#endif
+#if PP3_MLP_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+void policy_mlp(pp3pol::KNet* net, const float* obs, int obs_stride, float* act, int n, int row0,
+                pp3pol::LdsTileBuf* buf) {
+  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf>(*net, obs, obs_stride, act, NU, n, row0, *buf,
+                                                                       threadIdx.x);
+}
+
 template <int NC, bool FUSED, int NWV = 1>
 __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     typename std::conditional<(NWV > 1), PolicyStepArgs, StepArgs>::type a_arg) {
@@ -2208,9 +2228,9 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     const GPArgs& pa = *(const GPArgs*)ap;
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    mlp_tile(pa.net, a.obs_out, PP3_OBS_DIM * ((const DevModel*)(const GModel*)a.m)->H,
-             pa.act + (size_t)it * a.act_stride, NU, a.N, blockIdx.x * pp3pol::TILE, *reinterpret_cast<pp3pol::TileBuf*>(sh),
-             threadIdx.x);
+    policy_mlp(&pa.net, a.obs_out, PP3_OBS_DIM * ((const DevModel*)(const GModel*)a.m)->H,
+               pa.act + (size_t)it * a.act_stride, a.N, blockIdx.x * pp3pol::TILE,
+               (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)));
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   int lane = NWV > 1 ? (int)(threadIdx.x & (WAVE - 1)) : (int)threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)

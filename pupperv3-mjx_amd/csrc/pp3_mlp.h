@@ -41,6 +41,7 @@ struct Net {
 
 // LDS activations of one tile: two buffers of [TILE][MAXW + 4] floats (74 KB)
 typedef float TileBuf[2][TILE][MAXW + 4];
+typedef __attribute__((address_space(3))) float LdsTileBuf[2][TILE][MAXW + 4];  // (explicitly LDS)
 constexpr size_t TILE_BUF_BYTES = sizeof(TileBuf);
 
 __device__ __forceinline__ float activate(float x, int act) {
@@ -59,15 +60,41 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // so the layer records are scalar loads)
 typedef __attribute__((address_space(4))) const Net KNet;
 
+// One chunk (CG groups of 4 k-blocks) of tile t's B fragments, starting at group g0 (groups past
+// ngrp read as zero)
+__device__ __forceinline__ void load_chunk(const Layer& L, int t, int g0, int lane, f32x4 (&bq)[CG]) {
+  const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
+#pragma unroll
+  for (int q = 0; q < CG; q++) bq[q] = (g0 + q < L.ngrp) ? wf[(size_t)q * 64] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+template <class NetT>
+__device__ __forceinline__ Layer layer_of(NetT& net, int li) {
+  Layer L;  // (field by field: a constant-address-space record has no copy constructor)
+  L.w = net.layer[li].w; L.b = net.layer[li].b; L.K = net.layer[li].K; L.Kp = net.layer[li].Kp;
+  L.M = net.layer[li].M; L.Mp = net.layer[li].Mp; L.act = net.layer[li].act; L.ngrp = net.layer[li].ngrp;
+  return L;
+}
+
 // The MLP of observation rows row0 .. row0+15 (rows >= n read as zero, get no action) ->
 // act[row * act_stride + col] for col < out_dim.  Called by all 64 * NWAVE threads of the
 // workgroup (tid = threadIdx.x); `buf` is the workgroup's LDS scratch.  Ends with a barrier.
-// NetT: Net (a kernel's by-value argument) or KNet.
-template <class NetT>
+// NetT: Net (a kernel's by-value argument) or KNet.  PF (the fused rollout, which has the
+// registers): every weight chunk's loads are issued one chunk ahead -- the next chunk of the
+// tile, else the next tile's first, else the first chunk of this wave's first tile in the next
+// layer, across the epilogue and barrier -- and the very first before the observation tile is
+// staged.  Only the issue points of loads move: the MFMA sequence, and so the result, is the
+// same with and without.
+template <class NetT, bool PF = false, class BufT = TileBuf>
 __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ obs, int obs_stride,
-                                         float* __restrict__ act, int act_stride, int n, int row0, TileBuf& buf,
+                                         float* __restrict__ act, int act_stride, int n, int row0, BufT& buf,
                                          int tid) {
   const int lane = tid & 63, wave = tid >> 6;
+  f32x4 nxt[CG];  // PF: the next chunk's B fragments, in flight
+  if (PF) {
+    const Layer L0 = layer_of(net, 0);
+    if (wave < L0.Mp / TILE) load_chunk(L0, wave, 0, lane, nxt);
+  }
   // observation tile -> LDS (rows past n are zero)
   for (int i = tid; i < TILE * net.layer[0].Kp; i += 64 * NWAVE) {
     const int r = i / net.layer[0].Kp, k = i - r * net.layer[0].Kp;
@@ -77,11 +104,9 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
   __syncthreads();
   int cur = 0;
   for (int li = 0; li < net.n_layers; li++) {
-    Layer L;  // (field by field: a constant-address-space record has no copy constructor)
-    L.w = net.layer[li].w; L.b = net.layer[li].b; L.K = net.layer[li].K; L.Kp = net.layer[li].Kp;
-    L.M = net.layer[li].M; L.Mp = net.layer[li].Mp; L.act = net.layer[li].act; L.ngrp = net.layer[li].ngrp;
-    const float(*X)[MAXW + 4] = buf[cur];
-    float(*Y)[MAXW + 4] = buf[cur ^ 1];
+    const Layer L = layer_of(net, li);
+    auto& X = buf[cur];
+    auto& Y = buf[cur ^ 1];
     const int ntile = L.Mp / TILE;
     const bool last = li == net.n_layers - 1;
     for (int t = wave; t < ntile; t += NWAVE) {
@@ -93,16 +118,28 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
       for (int g0 = 0; g0 < L.ngrp; g0 += CG) {
         f32x4 bq[CG];
         float av[CG][4];
-        const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
+        if (PF) {
 #pragma unroll
-        for (int q = 0; q < CG; q++) {  // every load of the chunk in flight together
-          bq[q] = (g0 + q < L.ngrp) ? wf[(size_t)q * 64] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          for (int q = 0; q < CG; q++) bq[q] = nxt[q];
+          // the next chunk: this tile's, the next tile's of this layer, or the next layer's first
+          if (g0 + CG < L.ngrp) {
+            load_chunk(L, t, g0 + CG, lane, nxt);
+          } else if (t + NWAVE < ntile) {
+            load_chunk(L, t + NWAVE, 0, lane, nxt);
+          } else if (!last) {
+            const Layer Ln = layer_of(net, li + 1);
+            if (wave < Ln.Mp / TILE) load_chunk(Ln, wave, 0, lane, nxt);
+          }
+        } else {
+          load_chunk(L, t, g0, lane, bq);  // every load of the chunk in flight together
+        }
+#pragma unroll
+        for (int q = 0; q < CG; q++)
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             const int kb = 4 * (g0 + q) + j;
             av[q][j] = kb < nblk ? X[ar][4 * kb + kk] : 0.0f;
           }
-        }
 #pragma unroll
         for (int q = 0; q < CG; q++) {
           if (g0 + q < L.ngrp) {  // uniform; padded blocks of a ragged group multiply zeros
