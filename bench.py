@@ -40,7 +40,7 @@ FP32_PEAK_TFLOPS = 157.3    # vector FP32 (spec)
 # sustains one per 4 cycles).  Transcendentals are counted at the plain rate (a lower bound).
 N_SIMD, CLOCK_HZ, VALU_CYC = 1024, 2.4e9, 2
 KERNEL_SOURCES = ("pupperv3-mjx_amd/csrc/pp3_env.hip", "pupperv3-mjx_amd/csrc/pp3_device.h",
-                  "pupperv3-mjx_amd/csrc/Makefile")
+                  "pupperv3-mjx_amd/csrc/pp3_mlp.h", "pupperv3-mjx_amd/csrc/Makefile")
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_current.json")
 
 
@@ -772,7 +772,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": ("pp3::env_step_kernel<8, true, 8> (policy MLP fused)" if fused_policy else
-                                    "pp3::env_step_kernel<%d, %s>" % (env.config_struct.ncon_max or 8, "true" if rollout else "false")),
+                                    "pp3::env_step_kernel<%d, %s, 1>" % (env.config_struct.ncon_max or 8, "true" if rollout else "false")),
                          "steps_per_launch": spl, "bytes_per_env_step": bpe,
                          "algorithmic_bytes_per_launch": bpe * E * spl,
                          "launch_ms": round(launch_s * spl * 1e3, 4),

@@ -2188,6 +2188,22 @@ void policy_mlp(pp3pol::KNet* net, const float* obs, int obs_stride, float* act,
   pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf>(*net, obs, obs_stride, act, NU, n, row0, *buf,
                                                                        threadIdx.x);
 }
+// The same with the observation rows already in the workgroup's LDS tile (observation_history
+// <= 2: 36H <= OBS_TILE_W - 4 floats per row), written by the env steps themselves
+constexpr int OBS_TILE_W = 2 * PP3_OBS_DIM + 4;
+typedef __attribute__((address_space(3))) float LdsObsTile[pp3pol::TILE][OBS_TILE_W];
+#if PP3_MLP_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::LdsTileBuf* buf, LdsObsTile* in) {
+  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf, LdsObsTile>(*net, nullptr, 0, act, NU, n, row0,
+                                                                                   *buf, threadIdx.x, in);
+}
+#ifndef PP3_MLP_OBS_LDS
+#define PP3_MLP_OBS_LDS 1
+#endif
 
 template <int NC, bool FUSED, int NWV = 1>
 __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
@@ -2195,6 +2211,9 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   static_assert(NWV == 1 || (FUSED && NWV == pp3pol::NWAVE), "the policy rollout is fused, one MLP tile per workgroup");
   __shared__ Shared<NC> sh[2 * NWV];
   static_assert(NWV == 1 || sizeof(sh) >= pp3pol::TILE_BUF_BYTES, "the MLP's LDS scratch aliases the envs' blocks");
+  // the policy rollout's observation tile (its own LDS, next to the env blocks): each env step
+  // writes its env's new observation row into it, the next step's MLP reads it in place
+  __shared__ float obs_tile[NWV > 1 ? pp3pol::TILE : 1][OBS_TILE_W];
   int nsteps;
   if constexpr (NWV > 1) nsteps = a_arg.s.nsteps;
   else nsteps = FUSED ? a_arg.nsteps : 1;
@@ -2226,11 +2245,23 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     // (obs rows) visible; mlp_tile ends with one, after which the actions are visible.
     typedef __attribute__((address_space(4))) const PolicyStepArgs GPArgs;
     const GPArgs& pa = *(const GPArgs*)ap;
+    const int Hm = ((const DevModel*)(const GModel*)a.m)->H;
+    const bool tile_in = PP3_MLP_OBS_LDS && PP3_OBS_DIM * Hm + 4 <= OBS_TILE_W;
+    if (tile_in && it == 0) {  // first step of the launch: the observations come from global memory
+      for (int i = threadIdx.x; i < pp3pol::TILE * PP3_OBS_DIM * Hm; i += WAVE * NWV) {
+        const int r = i / (PP3_OBS_DIM * Hm), k = i - r * (PP3_OBS_DIM * Hm);
+        const int row = blockIdx.x * pp3pol::TILE + r;
+        obs_tile[r][k] = row < a.N ? a.obs_out[(size_t)row * (PP3_OBS_DIM * Hm) + k] : 0.0f;
+      }
+    }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    policy_mlp(&pa.net, a.obs_out, PP3_OBS_DIM * ((const DevModel*)(const GModel*)a.m)->H,
-               pa.act + (size_t)it * a.act_stride, a.N, blockIdx.x * pp3pol::TILE,
-               (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)));
+    if (tile_in)
+      policy_mlp_tile(&pa.net, pa.act + (size_t)it * a.act_stride, a.N, blockIdx.x * pp3pol::TILE,
+                      (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)), (LdsObsTile*)obs_tile);
+    else
+      policy_mlp(&pa.net, a.obs_out, PP3_OBS_DIM * Hm, pa.act + (size_t)it * a.act_stride, a.N,
+                 blockIdx.x * pp3pol::TILE, (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)));
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   int lane = NWV > 1 ? (int)(threadIdx.x & (WAVE - 1)) : (int)threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)
@@ -2295,6 +2326,8 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     for (int t = 0; t < OBS_MOVE; t++)
       if (l + HW * t < nmove) {
         oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
+        if constexpr (NWV > 1)
+          if (PP3_MLP_OBS_LDS && PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][PP3_OBS_DIM + l + HW * t] = tmp[t];
         if (TG && to) to[PP3_OBS_DIM + l + HW * t] = tmp[t];
       }
 #pragma unroll
@@ -2388,6 +2421,8 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     if (own)
       for (int k = l; k < PP3_OBS_DIM; k += HW) {
         oo[k] = s.x.e.o[k];
+        if constexpr (NWV > 1)
+          if (PP3_MLP_OBS_LDS && PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][k] = s.x.e.o[k];
         if (TG && to) to[k] = s.x.e.o[k];
       }
   }
@@ -2568,6 +2603,8 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     if (own)
       for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) {
         oo[i] = fo[i];
+        if constexpr (NWV > 1)
+          if (PP3_MLP_OBS_LDS && PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][i] = fo[i];
         if (TG && to) to[i] = fo[i];
       }
   }

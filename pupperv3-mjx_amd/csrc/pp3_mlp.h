@@ -41,6 +41,7 @@ struct Net {
 
 // LDS activations of one tile: two buffers of [TILE][MAXW + 4] floats (74 KB)
 typedef float TileBuf[2][TILE][MAXW + 4];
+typedef float TileRows[TILE][MAXW + 4];  // one of the two
 typedef __attribute__((address_space(3))) float LdsTileBuf[2][TILE][MAXW + 4];  // (explicitly LDS)
 constexpr size_t TILE_BUF_BYTES = sizeof(TileBuf);
 
@@ -84,31 +85,32 @@ __device__ __forceinline__ Layer layer_of(NetT& net, int li) {
 // tile, else the next tile's first, else the first chunk of this wave's first tile in the next
 // layer, across the epilogue and barrier -- and the very first before the observation tile is
 // staged.  Only the issue points of loads move: the MFMA sequence, and so the result, is the
-// same with and without.
-template <class NetT, bool PF = false, class BufT = TileBuf>
+// same with and without.  `in` (InT = float[TILE][W] in LDS, W >= in_dim, in_dim a multiple of
+// 4): the observation rows are already there (written by the env step, a barrier since), so the
+// first layer reads them in place instead of staging `obs` from global memory; rows past n may
+// hold anything (a row's outputs depend on that row only, and they are not stored).
+template <class NetT, bool PF = false, class BufT = TileBuf, class InT = TileRows>
 __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ obs, int obs_stride,
                                          float* __restrict__ act, int act_stride, int n, int row0, BufT& buf,
-                                         int tid) {
+                                         int tid, InT* in = nullptr) {
   const int lane = tid & 63, wave = tid >> 6;
   f32x4 nxt[CG];  // PF: the next chunk's B fragments, in flight
   if (PF) {
     const Layer L0 = layer_of(net, 0);
     if (wave < L0.Mp / TILE) load_chunk(L0, wave, 0, lane, nxt);
   }
-  // observation tile -> LDS (rows past n are zero)
-  for (int i = tid; i < TILE * net.layer[0].Kp; i += 64 * NWAVE) {
-    const int r = i / net.layer[0].Kp, k = i - r * net.layer[0].Kp;
-    const int row = row0 + r;
-    buf[0][r][k] = (row < n && k < net.in_dim) ? obs[(size_t)row * obs_stride + k] : 0.0f;
+  if (!in) {
+    // observation tile -> LDS (rows past n are zero)
+    for (int i = tid; i < TILE * net.layer[0].Kp; i += 64 * NWAVE) {
+      const int r = i / net.layer[0].Kp, k = i - r * net.layer[0].Kp;
+      const int row = row0 + r;
+      buf[0][r][k] = (row < n && k < net.in_dim) ? obs[(size_t)row * obs_stride + k] : 0.0f;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  int cur = 0;
-  for (int li = 0; li < net.n_layers; li++) {
-    const Layer L = layer_of(net, li);
-    auto& X = buf[cur];
-    auto& Y = buf[cur ^ 1];
+  // one layer's output tiles of this wave: X the [TILE][.] input rows, Y the output rows
+  auto layer = [&](auto& X, auto& Y, const Layer& L, int li, bool last) {
     const int ntile = L.Mp / TILE;
-    const bool last = li == net.n_layers - 1;
     for (int t = wave; t < ntile; t += NWAVE) {
       const int c0 = t * TILE;
       // two independent accumulators (even / odd k blocks) cover the dependent MFMA latency
@@ -165,6 +167,13 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
       }
     }
     __syncthreads();
+  };
+  int cur = 0;
+  for (int li = 0; li < net.n_layers; li++) {
+    const Layer L = layer_of(net, li);
+    const bool last = li == net.n_layers - 1;
+    if (li == 0 && in) layer(*in, buf[1], L, li, last);
+    else layer(buf[cur], buf[cur ^ 1], L, li, last);
     cur ^= 1;
   }
 }

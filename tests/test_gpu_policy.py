@@ -100,3 +100,43 @@ def test_rollout_policy_equals_act_then_step(require_gpu, tmp_path, n, sizes, H)
         ab.free(); dp.close()
         for e in envs:
             e.close()
+
+
+def test_rollout_policy_with_dr_and_terrain_equals_act_then_step(require_gpu, tmp_path):
+    """The fused policy rollout on domain-randomised envs (each env its own DR row) standing on
+    per-env terrain (the sphere-box lanes index the terrain rows by env, with 16 envs per
+    workgroup here): bit-equal to the per-step policy + step launches."""
+    from pupperv3_mjx import domain_randomization, rng
+    path = common.write_model(tmp_path, 10)
+    n, K = 40, 10
+    envs = [PupperV3Env(**common.fixture_kwargs(path), num_envs=n) for _ in range(2)]
+    pol = _policy([72, 256, 128, 128, 24], "elu")
+    dp = export.DevicePolicy(pol)
+    ab = _lib.DeviceBuffer(n * 12 * 4)
+    try:
+        sysb, _ = domain_randomization.domain_randomize(envs[0].sys, rng.split(rng.PRNGKey(3), n))
+        states = []
+        for e in envs:
+            e.set_domain_randomization(sysb)
+            st = e.reset(make_keys(4, n))
+            xy = st._record[:, _abi.S_QPOS:_abi.S_QPOS + 2].astype(np.float64)
+            e.set_terrain(common.terrain_under(xy, 10, seed=5))
+            states.append(st)
+        s1, tr = envs[0].rollout_policy(states[0], dp, K)
+        s2 = states[1]
+        acts = []
+        for _ in range(K):
+            dp.act_env(envs[1], ab.ptr.value)
+            a = np.zeros((n, 12), dtype=np.float32)
+            envs[1].synchronize()
+            _lib.check(_lib.load().pp3_memcpy_d2h(a.ctypes.data_as(C.c_void_p), ab.ptr, a.nbytes))
+            s2 = envs[1].step(s2, a)
+            acts.append(a)
+        np.testing.assert_array_equal(tr["action"], np.stack(acts))
+        np.testing.assert_array_equal(s1._record, s2._record)
+        np.testing.assert_array_equal(s1.obs, s2.obs)
+        assert s1.pipeline_state.contact.ncon.sum() > 0
+    finally:
+        ab.free(); dp.close()
+        for e in envs:
+            e.close()

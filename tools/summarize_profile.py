@@ -20,7 +20,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNEL = "env_step_kernel<8, true>"
+KERNEL = "env_step_kernel<8, true, 1>"  # (the fused policy rollout is <8, true, 8>)
 
 
 def _arg(name, default):
@@ -28,7 +28,8 @@ def _arg(name, default):
 
 
 def _kernel():
-    return "env_step_kernel<8, false>" if _arg("--launch", "rollout") == "step" else KERNEL
+    launch = _arg("--launch", "rollout")
+    return {"step": "env_step_kernel<8, false, 1>", "policy": "env_step_kernel<8, true, 8>"}.get(launch, KERNEL)
 
 
 def _pmc(d):
@@ -43,7 +44,7 @@ def _pmc(d):
                 per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     if not per:
         return {}
-    if _arg("--launch", "rollout") == "rollout":
+    if _arg("--launch", "rollout") in ("rollout", "policy"):
         return dict(per[max(per)])
     agg = defaultdict(list)
     for c in per.values():
@@ -68,7 +69,7 @@ def _trace_last(d):
 def main():
     d = sys.argv[1]
     launch = _arg("--launch", "rollout")
-    spl = int(_arg("--steps-per-launch", 50 if launch == "rollout" else 1))  # gpu_profile.sh: --steps 50
+    spl = int(_arg("--steps-per-launch", 50 if launch in ("rollout", "policy") else 1))  # gpu_profile.sh: --steps 50
     out = {"kernel": _kernel(), "launch": launch, "steps_per_launch": spl}
     stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
@@ -76,7 +77,7 @@ def main():
             if _kernel() in r["Name"]:
                 out["kernel_avg_ns"] = float(r["AverageNs"])
                 out["kernel_calls"] = int(r["Calls"])
-    if launch == "rollout":
+    if launch in ("rollout", "policy"):
         t = _trace_last(d)
         if t is not None:  # the timed window's launch (the stats' average includes the pre-warm's)
             out["kernel_avg_ns"] = t
