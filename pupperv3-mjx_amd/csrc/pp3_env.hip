@@ -2204,6 +2204,18 @@ void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::Lds
 #ifndef PP3_MLP_OBS_LDS
 #define PP3_MLP_OBS_LDS 1
 #endif
+// Between the fused steps every global value a wave reads back was stored by a wave of the same
+// workgroup, so on the same CU.  PP3_STEP_ACQ_AGENT=1 (the round-3 form) acquires at agent scope
+// (buffer_inv sc1: the whole vector L1 dropped every step); 0 at workgroup scope, which the
+// gfx942/950 memory model (non-tgsplit) serves from the CU's own L1 without an invalidate.
+#ifndef PP3_STEP_ACQ_AGENT
+#define PP3_STEP_ACQ_AGENT 1
+#endif
+#if PP3_STEP_ACQ_AGENT
+#define PP3_STEP_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#else
+#define PP3_STEP_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
+#endif
 
 template <int NC, bool FUSED, int NWV = 1>
 __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
@@ -2255,14 +2267,14 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
       }
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    PP3_STEP_ACQUIRE();
     if (tile_in)
       policy_mlp_tile(&pa.net, pa.act + (size_t)it * a.act_stride, a.N, blockIdx.x * pp3pol::TILE,
                       (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)), (LdsObsTile*)obs_tile);
     else
       policy_mlp(&pa.net, a.obs_out, PP3_OBS_DIM * Hm, pa.act + (size_t)it * a.act_stride, a.N,
                  blockIdx.x * pp3pol::TILE, (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)));
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    PP3_STEP_ACQUIRE();
   }
   int lane = NWV > 1 ? (int)(threadIdx.x & (WAVE - 1)) : (int)threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)
   if (FUSED) asm volatile("" : "+v"(lane));
@@ -2619,7 +2631,7 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   if (!FUSED || ++it >= nsteps) break;
   // the next step reads back this step's global stores (state record, lag rows, obs history)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  PP3_STEP_ACQUIRE();
   }
 #ifdef PP3_PHASE_PROF
   static_assert(NWV == 1, "the per-wave profile records index waves by workgroup");
