@@ -3482,6 +3482,8 @@ int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float
   if (nsteps < 1) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: nsteps must be >= 1");
   if (pp3_policy_out_dim(policy) != NU) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: the policy must have 12 outputs");
   if (pp3_policy_device(policy) != e->device) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: policy and env on different devices");
+  if (pp3_policy_net(policy)->in_dim != PP3_OBS_DIM * e->H)
+    return set_err(PP3_ERR_ARG, "pp3_rollout_policy: the policy's input width must equal the observation size 36 * observation_history");
   const size_t on = (size_t)e->N * PP3_OBS_DIM * e->H;
   const hipStream_t st = stream_of(e, stream);
   const int repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;

@@ -23,7 +23,11 @@ the answers come from mechanics and from MuJoCo's documented constraint model):
 Pyramidal contact friction with impratio (the edge rows' regulariser and the one-Newton-iteration
 response) is pinned in tests/test_friction_kat.py on a body that cannot tip (a solid ball on a
 slope: the exact soft-pyramid minimiser, rolling at 5/7 g sin, the Coulomb bound, impratio creep),
-and on the kernel by tests/test_gpu_kat.py.  What stays unpinned is MuJoCo's own implementation
+and on the kernel by tests/test_gpu_kat.py.  solref/solimp MIXING (the collision class, xml:51,
+against the floor's defaults, xml:219: resting depth, steady rolling creep, converged qacc) and the
+pyramid's TANGENT BASIS for normals off the vertical (mju_makeFrame on tilted box faces, edges,
+corners and between two legs' spheres) are pinned in tests/test_contact_kat.py (oracle) and
+tests/test_gpu_contact_kat.py (kernel), from MuJoCo's documentation (tests/contact_kat.py).  What stays unpinned is MuJoCo's own implementation
 (both restatements are checked against its documented constraint model, not its C source).
 """
 import numpy as np
