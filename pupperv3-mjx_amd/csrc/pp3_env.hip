@@ -2173,7 +2173,7 @@ struct PolicyStepArgs {
 // registers are allocated on their own instead of shaping the env step's allocation around it
 // (inlined, the fused kernel spilled 17 VGPRs; the step alone spills none).
 #ifndef PP3_MLP_PF
-#define PP3_MLP_PF 1
+#define PP3_MLP_PF 0  // (measured: one-chunk-ahead prefetch +3 us per step)
 #endif
 #ifndef PP3_MLP_NOINLINE
 #define PP3_MLP_NOINLINE 1
@@ -2205,11 +2205,13 @@ void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::Lds
 #define PP3_MLP_OBS_LDS 1
 #endif
 // Between the fused steps every global value a wave reads back was stored by a wave of the same
-// workgroup, so on the same CU.  PP3_STEP_ACQ_AGENT=1 (the round-3 form) acquires at agent scope
-// (buffer_inv sc1: the whole vector L1 dropped every step); 0 at workgroup scope, which the
-// gfx942/950 memory model (non-tgsplit) serves from the CU's own L1 without an invalidate.
+// workgroup (the env step: by the same lane), so on the same CU.  PP3_STEP_ACQ_AGENT=1 (the
+// round-3 form) acquires at agent scope (buffer_inv sc1: the whole vector L1 dropped every step);
+// 0 (default) at workgroup scope, which the gfx942/950 memory model (non-tgsplit) serves from the
+// CU's own L1 without an invalidate: equal end states, +0.4 % on the env rollout, and the policy
+// rollout's three per-step acquires cost 35 us per step at agent scope.
 #ifndef PP3_STEP_ACQ_AGENT
-#define PP3_STEP_ACQ_AGENT 1
+#define PP3_STEP_ACQ_AGENT 0
 #endif
 #if PP3_STEP_ACQ_AGENT
 #define PP3_STEP_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
@@ -2266,15 +2268,24 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
         obs_tile[r][k] = row < a.N ? a.obs_out[(size_t)row * (PP3_OBS_DIM * Hm) + k] : 0.0f;
       }
     }
-    __syncthreads();
-    PP3_STEP_ACQUIRE();
-    if (tile_in)
-      policy_mlp_tile(&pa.net, pa.act + (size_t)it * a.act_stride, a.N, blockIdx.x * pp3pol::TILE,
-                      (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)), (LdsObsTile*)obs_tile);
-    else
-      policy_mlp(&pa.net, a.obs_out, PP3_OBS_DIM * Hm, pa.act + (size_t)it * a.act_stride, a.N,
-                 blockIdx.x * pp3pol::TILE, (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)));
-    PP3_STEP_ACQUIRE();
+#ifndef PP3_MLP_SKIP
+#define PP3_MLP_SKIP 0  // timing diagnostics only: 1 = no MLP (barriers kept), 2 = no MLP, no barriers
+#endif
+    if (PP3_MLP_SKIP < 2) {
+      __syncthreads();
+      PP3_STEP_ACQUIRE();
+    }
+    if (PP3_MLP_SKIP == 0) {
+      if (tile_in)
+        policy_mlp_tile(&pa.net, pa.act + (size_t)it * a.act_stride, a.N, blockIdx.x * pp3pol::TILE,
+                        (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)), (LdsObsTile*)obs_tile);
+      else
+        policy_mlp(&pa.net, a.obs_out, PP3_OBS_DIM * Hm, pa.act + (size_t)it * a.act_stride, a.N,
+                   blockIdx.x * pp3pol::TILE, (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)));
+      PP3_STEP_ACQUIRE();
+    } else if (PP3_MLP_SKIP == 1) {
+      __syncthreads();
+    }
   }
   int lane = NWV > 1 ? (int)(threadIdx.x & (WAVE - 1)) : (int)threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)
   if (FUSED) asm volatile("" : "+v"(lane));

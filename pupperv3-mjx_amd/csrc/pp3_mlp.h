@@ -61,19 +61,43 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // so the layer records are scalar loads)
 typedef __attribute__((address_space(4))) const Net KNet;
 
+#ifndef PP3_MLP_DIAG
+#define PP3_MLP_DIAG 0  // timing diagnostics only (wrong results): 1 identity activations, 2 every chunk
+#endif                  // reads tile 0's first chunk (L1-resident weights), 4 no MFMA, 8 no barriers
 // One chunk (CG groups of 4 k-blocks) of tile t's B fragments, starting at group g0 (groups past
 // ngrp read as zero)
 __device__ __forceinline__ void load_chunk(const Layer& L, int t, int g0, int lane, f32x4 (&bq)[CG]) {
+  if (PP3_MLP_DIAG & 2) { t = 0; g0 = 0; }
   const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
 #pragma unroll
   for (int q = 0; q < CG; q++) bq[q] = (g0 + q < L.ngrp) ? wf[(size_t)q * 64] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
+// wave-uniform values kept in SGPRs: an out-of-line caller passes them in VGPRs (the function ABI),
+// which would make every loop bound and predicate below look divergent (exec-mask branches
+// around each load); readfirstlane of a value already in an SGPR is free
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <class T>
+__device__ __forceinline__ T* uni(T* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// the same for a chunk that lies wholly inside the layer (no predicates)
+__device__ __forceinline__ void load_chunk_full(const Layer& L, int t, int g0, int lane, f32x4 (&bq)[CG]) {
+  if (PP3_MLP_DIAG & 2) { t = 0; g0 = 0; }
+  const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
+#pragma unroll
+  for (int q = 0; q < CG; q++) bq[q] = wf[(size_t)q * 64];
+}
+
 template <class NetT>
 __device__ __forceinline__ Layer layer_of(NetT& net, int li) {
   Layer L;  // (field by field: a constant-address-space record has no copy constructor)
-  L.w = net.layer[li].w; L.b = net.layer[li].b; L.K = net.layer[li].K; L.Kp = net.layer[li].Kp;
-  L.M = net.layer[li].M; L.Mp = net.layer[li].Mp; L.act = net.layer[li].act; L.ngrp = net.layer[li].ngrp;
+  L.w = uni(net.layer[li].w); L.b = uni(net.layer[li].b); L.K = uni(net.layer[li].K); L.Kp = uni(net.layer[li].Kp);
+  L.M = uni(net.layer[li].M); L.Mp = uni(net.layer[li].Mp); L.act = uni(net.layer[li].act);
+  L.ngrp = uni(net.layer[li].ngrp);
   return L;
 }
 
@@ -93,7 +117,13 @@ template <class NetT, bool PF = false, class BufT = TileBuf, class InT = TileRow
 __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ obs, int obs_stride,
                                          float* __restrict__ act, int act_stride, int n, int row0, BufT& buf,
                                          int tid, InT* in = nullptr) {
-  const int lane = tid & 63, wave = tid >> 6;
+  // the wave index is wave-uniform: readfirstlane says so, so the tile / chunk / group loops below
+  // become scalar branches instead of exec-mask divergence
+  const int lane = tid & 63, wave = uni(tid >> 6);
+  n = uni(n);
+  row0 = uni(row0);
+  act = uni(act);
+  act_stride = uni(act_stride);
   f32x4 nxt[CG];  // PF: the next chunk's B fragments, in flight
   if (PF) {
     const Layer L0 = layer_of(net, 0);
@@ -101,10 +131,13 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
   }
   if (!in) {
     // observation tile -> LDS (rows past n are zero)
-    for (int i = tid; i < TILE * net.layer[0].Kp; i += 64 * NWAVE) {
-      const int r = i / net.layer[0].Kp, k = i - r * net.layer[0].Kp;
+    const int kp0 = uni(net.layer[0].Kp), in_dim = uni(net.in_dim);
+    obs = uni(obs);
+    obs_stride = uni(obs_stride);
+    for (int i = tid; i < TILE * kp0; i += 64 * NWAVE) {
+      const int r = i / kp0, k = i - r * kp0;
       const int row = row0 + r;
-      buf[0][r][k] = (row < n && k < net.in_dim) ? obs[(size_t)row * obs_stride + k] : 0.0f;
+      buf[0][r][k] = (row < n && k < in_dim) ? obs[(size_t)row * obs_stride + k] : 0.0f;
     }
     __syncthreads();
   }
@@ -113,11 +146,16 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
     const int ntile = L.Mp / TILE;
     for (int t = wave; t < ntile; t += NWAVE) {
       const int c0 = t * TILE;
+      const int col = c0 + (lane & 15);
+      const float bias = L.b[col];  // (issued before the weight chunks: its wait never waits for them)
       // two independent accumulators (even / odd k blocks) cover the dependent MFMA latency
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
       const int ar = lane & 15, kk = lane >> 4;
       const int nblk = L.Kp / 4;
       for (int g0 = 0; g0 < L.ngrp; g0 += CG) {
+        // a whole chunk (every group and k block inside the layer) runs without per-element
+        // predicates; the ragged last chunk keeps them.  The MFMA sequence is the same either way.
+        const bool full = g0 + CG <= L.ngrp && 4 * (g0 + CG) <= nblk;
         f32x4 bq[CG];
         float av[CG][4];
         if (PF) {
@@ -132,19 +170,31 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
             const Layer Ln = layer_of(net, li + 1);
             if (wave < Ln.Mp / TILE) load_chunk(Ln, wave, 0, lane, nxt);
           }
+        } else if (full) {
+          load_chunk_full(L, t, g0, lane, bq);
         } else {
           load_chunk(L, t, g0, lane, bq);  // every load of the chunk in flight together
         }
+        if (full) {
 #pragma unroll
-        for (int q = 0; q < CG; q++)
+          for (int q = 0; q < CG; q++)
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int kb = 4 * (g0 + q) + j;
-            av[q][j] = kb < nblk ? X[ar][4 * kb + kk] : 0.0f;
-          }
+            for (int j = 0; j < 4; j++) av[q][j] = X[ar][4 * (4 * (g0 + q) + j) + kk];
+        } else {
+#pragma unroll
+          for (int q = 0; q < CG; q++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const int kb = 4 * (g0 + q) + j;
+              av[q][j] = kb < nblk ? X[ar][4 * kb + kk] : 0.0f;
+            }
+        }
 #pragma unroll
         for (int q = 0; q < CG; q++) {
-          if (g0 + q < L.ngrp) {  // uniform; padded blocks of a ragged group multiply zeros
+          if (PP3_MLP_DIAG & 4) {
+            acc[0] += av[q][0] * bq[q].x + av[q][2] * bq[q].z;
+            acc1[0] += av[q][1] * bq[q].y + av[q][3] * bq[q].w;
+          } else if (full || g0 + q < L.ngrp) {  // uniform; padded blocks of a ragged group multiply zeros
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][0], bq[q].x, acc, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][1], bq[q].y, acc1, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][2], bq[q].z, acc, 0, 0, 0);
@@ -153,12 +203,10 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
         }
       }
       acc += acc1;
-      const int col = c0 + (lane & 15);
-      const float bias = L.b[col];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = 4 * (lane >> 4) + r;
-        const float v = activate(acc[r] + bias, L.act);
+        const float v = (PP3_MLP_DIAG & 1) ? acc[r] + bias : activate(acc[r] + bias, L.act);
         if (!last) {
           Y[row][col] = v;
         } else if (col < L.M && row0 + row < n) {
@@ -166,12 +214,13 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
         }
       }
     }
-    __syncthreads();
+    if (!(PP3_MLP_DIAG & 8)) __syncthreads();
   };
   int cur = 0;
-  for (int li = 0; li < net.n_layers; li++) {
+  const int n_layers = uni(net.n_layers);
+  for (int li = 0; li < n_layers; li++) {
     const Layer L = layer_of(net, li);
-    const bool last = li == net.n_layers - 1;
+    const bool last = li == n_layers - 1;
     if (li == 0 && in) layer(*in, buf[1], L, li, last);
     else layer(buf[cur], buf[cur ^ 1], L, li, last);
     cur ^= 1;
