@@ -2178,6 +2178,9 @@ struct PolicyStepArgs {
 #ifndef PP3_MLP_NOINLINE
 #define PP3_MLP_NOINLINE 1
 #endif
+#ifndef PP3_MLP_CG
+#define PP3_MLP_CG 4
+#endif
 #if PP3_MLP_NOINLINE
 __device__ __noinline__
 #else
@@ -2185,8 +2188,8 @@ __device__ __forceinline__
 #endif
 void policy_mlp(pp3pol::KNet* net, const float* obs, int obs_stride, float* act, int n, int row0,
                 pp3pol::LdsTileBuf* buf) {
-  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf>(*net, obs, obs_stride, act, NU, n, row0, *buf,
-                                                                       threadIdx.x);
+  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf, pp3pol::TileRows, PP3_MLP_CG>(
+      *net, obs, obs_stride, act, NU, n, row0, *buf, threadIdx.x);
 }
 // The same with the observation rows already in the workgroup's LDS tile (observation_history
 // <= 2: 36H <= OBS_TILE_W - 4 floats per row), written by the env steps themselves
@@ -2198,8 +2201,8 @@ __device__ __noinline__
 __device__ __forceinline__
 #endif
 void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::LdsTileBuf* buf, LdsObsTile* in) {
-  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf, LdsObsTile>(*net, nullptr, 0, act, NU, n, row0,
-                                                                                   *buf, threadIdx.x, in);
+  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf, LdsObsTile, PP3_MLP_CG>(
+      *net, nullptr, 0, act, NU, n, row0, *buf, threadIdx.x, in);
 }
 #ifndef PP3_MLP_OBS_LDS
 #define PP3_MLP_OBS_LDS 1

@@ -26,7 +26,7 @@ namespace pp3pol {
 constexpr int TILE = 16;                    // environments per tile (one workgroup)
 constexpr int NWAVE = 8;                    // waves per tile
 constexpr int MAXW = PP3_POLICY_MAX_WIDTH;  // widest layer (padded)
-constexpr int CG = 8;                       // groups of 4 k-blocks (32 k-blocks = 128 inputs) per chunk
+constexpr int CG8 = 8;                      // groups of 4 k-blocks (32 k-blocks = 128 inputs) per chunk
 
 struct Layer {
   const float* w;  // fragment order [Mp/16][ngrp][64 lanes][4], zero padded
@@ -66,6 +66,7 @@ typedef __attribute__((address_space(4))) const Net KNet;
 #endif                  // reads tile 0's first chunk (L1-resident weights), 4 no MFMA, 8 no barriers
 // One chunk (CG groups of 4 k-blocks) of tile t's B fragments, starting at group g0 (groups past
 // ngrp read as zero)
+template <int CG>
 __device__ __forceinline__ void load_chunk(const Layer& L, int t, int g0, int lane, f32x4 (&bq)[CG]) {
   if (PP3_MLP_DIAG & 2) { t = 0; g0 = 0; }
   const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
@@ -85,6 +86,7 @@ __device__ __forceinline__ T* uni(T* p) {
 }
 
 // the same for a chunk that lies wholly inside the layer (no predicates)
+template <int CG>
 __device__ __forceinline__ void load_chunk_full(const Layer& L, int t, int g0, int lane, f32x4 (&bq)[CG]) {
   if (PP3_MLP_DIAG & 2) { t = 0; g0 = 0; }
   const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
@@ -113,7 +115,10 @@ __device__ __forceinline__ Layer layer_of(NetT& net, int li) {
 // 4): the observation rows are already there (written by the env step, a barrier since), so the
 // first layer reads them in place instead of staging `obs` from global memory; rows past n may
 // hold anything (a row's outputs depend on that row only, and they are not stored).
-template <class NetT, bool PF = false, class BufT = TileBuf, class InT = TileRows>
+// CG: groups of 4 k-blocks per chunk (8 in the stand-alone kernel; the fused rollout's out-of-line
+// call uses 4, whose registers fit the callee's caller-saved VGPRs: no save / restore through
+// scratch per call).  The MFMA sequence does not depend on it.
+template <class NetT, bool PF = false, class BufT = TileBuf, class InT = TileRows, int CG = CG8>
 __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ obs, int obs_stride,
                                          float* __restrict__ act, int act_stride, int n, int row0, BufT& buf,
                                          int tid, InT* in = nullptr) {
