@@ -3501,6 +3501,7 @@ int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float
   const size_t on = (size_t)e->N * PP3_OBS_DIM * e->H;
   const hipStream_t st = stream_of(e, stream);
   const int repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;
+  (void)repeat;  // (the diagnostic build has no fused policy kernel)
 #ifndef PP3_PHASE_PROF
   if (e->nc == 8 && repeat == 1 && !g_policy_unfused) {
     // ONE launch for the K steps: 8-wave workgroups of 16 envs run the MLP (mlp_tile, the code of
