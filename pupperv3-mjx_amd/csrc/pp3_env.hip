@@ -465,8 +465,15 @@ __device__ __forceinline__ PairLoad load_pair(const DevModel& m, int p) {
   r.v[6] = *reinterpret_cast<const v4f*>(&m.pair_con[p]);
   return r;
 }
+// the per-env terrain table and its row length, read once per collision pass (above the
+// lane-divergent pair-kind branches, which would otherwise each re-issue both scalar loads, one
+// round trip after the other)
+struct TerrainRef {
+  uint64_t terrain;
+  int nbox;
+};
 template <int NC, int NWV = 1>
-__device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, PairLoad pl, float& dist, float pos[3],
+__device__ __forceinline__ bool narrow(const Shared<NC>& s, const TerrainRef& tr, PairLoad pl, float& dist, float pos[3],
                                        float nrm[3], v4f& pc0) {
   PairRec rec;
   {
@@ -509,11 +516,11 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const DevModel& m, P
     float R2[9], hh[3];
     for (int k = 0; k < 9; k++) R2[k] = rec.R[k];
     for (int k = 0; k < 3; k++) hh[k] = rec.half[k];
-    if (m.terrain) {  // per-env terrain: this env's box in slot -1 - s2 (rows padded to an even env count)
+    if (tr.terrain) {  // per-env terrain: this env's box in slot -1 - s2 (rows padded to an even env count)
       typedef float v4f __attribute__((ext_vector_type(4)));
       typedef __attribute__((address_space(1))) const v4f GF4;
       const int env_raw = 2 * NWV * blockIdx.x + (threadIdx.x >> 5);  // (NWV waves = 2 NWV envs per workgroup)
-      const GF4* t = (const GF4*)(uintptr_t)m.terrain + ((size_t)env_raw * m.nbox + (-1 - rec.s2)) * 4;
+      const GF4* t = (const GF4*)(uintptr_t)tr.terrain + ((size_t)env_raw * tr.nbox + (-1 - rec.s2)) * 4;
       const v4f t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
       p2[0] = t0.x; p2[1] = t0.y; p2[2] = t0.z;
       R2[0] = t0.w; R2[1] = t1.x; R2[2] = t1.y; R2[3] = t1.z; R2[4] = t1.w;
@@ -577,13 +584,14 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const v4f& pc0, int
 template <int NC, int NWV = 1>
 __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h, const PairLoad& pre) {
   int nhit = 0;
+  const TerrainRef tr{m.terrain, m.nbox};
   for (int base = 0; base < m.npair; base += HW) {
     const int p = base + l;
     float dist = 0, pos[3], nrm[3];
     v4f pc0;
     // the first 32 pairs' records were fetched at the substep start (they arrive during kinematics)
     const PairLoad pl = base == 0 ? pre : load_pair(m, p < m.npair ? p : 0);
-    const bool hit = narrow<NC, NWV>(s, m, pl, dist, pos, nrm, pc0) && (p < m.npair);
+    const bool hit = narrow<NC, NWV>(s, tr, pl, dist, pos, nrm, pc0) && (p < m.npair);
     const uint32_t mask = hballot(hit, h);
     const int slot = nhit + __popc(mask & ((1u << l) - 1u));
     if (hit) {
@@ -629,7 +637,7 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
       if (keep[t]) {
         float dist, pos[3], nrm[3];
         v4f pc0;
-        narrow<NC, NWV>(s, m, load_pair(m, keep_p[t]), dist, pos, nrm, pc0);
+        narrow<NC, NWV>(s, tr, load_pair(m, keep_p[t]), dist, pos, nrm, pc0);
         store_contact(s, pc0, slot[t], keep_p[t], dist, pos, nrm);
       }
     }
@@ -1190,17 +1198,22 @@ __device__ __forceinline__ void hess_acc(float (&a)[NV], const float (&J)[3][NV]
 // index drawn by jax.random.choice(p) from u = uniform(key): searchsorted_left(cumsum(p), cumsum[-1]*(1-u))
 // (n <= PP3_MAX_LAG; unrolled over the cap so the wave-uniform dist reads are one scalar load)
 __device__ __forceinline__ int choice_from_uniform(const GFloat* dist, int n, float u) {
+  // the whole (fixed-size) table first: one batch of scalar loads and one wait, not a load and a
+  // wait behind every `i < n` branch (16 serial round trips per call)
+  float d[PP3_MAX_LAG];
+#pragma unroll
+  for (int i = 0; i < PP3_MAX_LAG; i++) d[i] = dist[i];
   float total = 0.0f;
 #pragma unroll
   for (int i = 0; i < PP3_MAX_LAG; i++)
-    if (i < n) total += dist[i];
+    if (i < n) total += d[i];
   const float r = total * (1.0f - u);
   float acc = 0.0f;
   int li = 0;
 #pragma unroll
   for (int i = 0; i < PP3_MAX_LAG; i++)
     if (i < n) {
-      acc += dist[i];
+      acc += d[i];
       li += (acc < r) ? 1 : 0;
     }
   return li < n ? li : n - 1;
@@ -2578,6 +2591,13 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   // wrapper step is k launches with the same action; the reward is summed over them, and the
   // episode bookkeeping, done and the auto-reset happen at the last one
   const bool last = a.phase == a.repeat - 1;
+  // the output pointers read here, above the one-lane branches: read inside them, each is a
+  // scalar load and a wait of its own, one after the other
+  float* const o_reward = a.reward;
+  float* const o_done = a.done;
+  float* const o_metrics = a.metrics;
+  float* const o_treward = a.traj_reward;
+  float* const o_tdone = a.traj_done;
   float rout = reward;
   if (a.episode) {
     rout = reward + s.ep_racc;
@@ -2595,16 +2615,16 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     }
   }
   if (own && l == 0) {
-    a.reward[env] = rout;
-    if (!a.episode || last) a.done[env] = done_out ? 1.0f : 0.0f;
+    o_reward[env] = rout;
+    if (!a.episode || last) o_done[env] = done_out ? 1.0f : 0.0f;
     if (TG && (!a.episode || last)) {
-      if (a.traj_reward) a.traj_reward[(size_t)it * a.N + env] = rout;
-      if (a.traj_done) a.traj_done[(size_t)it * a.N + env] = done_out ? 1.0f : 0.0f;
+      if (o_treward) o_treward[(size_t)it * a.N + env] = rout;
+      if (o_tdone) o_tdone[(size_t)it * a.N + env] = done_out ? 1.0f : 0.0f;
     }
-    a.metrics[(size_t)env * PP3_NMETRIC] =
+    o_metrics[(size_t)env * PP3_NMETRIC] =
         sqrtf(s.xpos[tb][0] * s.xpos[tb][0] + s.xpos[tb][1] * s.xpos[tb][1] + s.xpos[tb][2] * s.xpos[tb][2]);
   }
-  if (own && l < PP3_NREWARD) a.metrics[(size_t)env * PP3_NMETRIC + 1 + l] = rmine;
+  if (own && l < PP3_NREWARD) o_metrics[(size_t)env * PP3_NMETRIC + 1 + l] = rmine;
   if (l < NU) {
     s.st[PP3_S_LAST_ACT + l] = act_in;
     s.st[PP3_S_LAST_VEL + l] = s.qvel[6 + l];
