@@ -2262,6 +2262,9 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   // and the kernel compiles to the single-step code it always was.
   int heavy_prev = 0;  // fused: the load flag carries over into the next step's first substep
   for (int it = 0;;) {
+#ifdef PP3_PHASE_PROF
+  if (it == 1) pf->n = 0;  // fused launch: the stamp trace holds the second step (a warm one)
+#endif
   const GArgs* ap = (const GArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   if (FUSED) asm volatile("" : "+s"(ap));
   const StepArgs* ap_step;
@@ -2311,7 +2314,12 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   const int env_raw = 2 * (blockIdx.x * NWV + wv) + h;
   const bool own = env_raw < a.N;
   const int env = own ? env_raw : a.N - 1;
-  const DevModel& m = *(const DevModel*)(const GModel*)a.m;  // constant AS: uniform reads -> s_load
+  // constant AS: uniform reads -> s_load.  Through a fresh opaque pointer, as in the epilogue: in
+  // the fused loop the kernel-level reference's reads were vector loads, five of them each waited
+  // for on its own (H, n_frames, La / Li, stride, imu_off: ~5 k cycles per step)
+  const GModel* mp_pro = (const GModel*)(a.m);
+  if (FUSED) asm volatile("" : "+s"(mp_pro));
+  const DevModel& m = *(const DevModel*)mp_pro;
   const int stride = m.stride;
   const int part = m.partitionable;
   float* gst = a.state + (size_t)env * stride;

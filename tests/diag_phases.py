@@ -2,7 +2,8 @@
 
 PP3_LIB_PATH=pupperv3-mjx_amd/pupperv3_mjx/libpupper_hip_prof.so python tests/diag_phases.py
 Stamps are s_memtime reads into per-wave registers (a few % overhead; each stamp drains the LDS
-reads in flight).
+reads in flight).  DIAG_FUSED=1 times one fused pp3_rollout launch instead of single-step launches
+(the per-wave stamp trace then holds the launch's second step; tools/trace_intervals.py).
 """
 import ctypes as C
 import os
@@ -41,7 +42,11 @@ def main():
     _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, warm, C.byref(ms)))
     buf = (C.c_uint64 * 22)()
     _lib.check(L.pp3_phase_profile(buf, 22, 1))
-    _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + warm * E * 48), E * 12, steps, C.byref(ms)))
+    if os.environ.get("DIAG_FUSED") == "1":  # one pp3_rollout launch (trace: its second step)
+        _lib.check(L.pp3_rollout_timed(env._h, C.c_void_p(acts.ptr.value + warm * E * 48), E * 12, steps,
+                                       None, None, None, C.byref(ms)))
+    else:
+        _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + warm * E * 48), E * 12, steps, C.byref(ms)))
     _lib.check(L.pp3_phase_profile(buf, 22, 1))
     v = np.array(buf[:len(NAMES)], dtype=np.float64)
     tot = v.sum()
