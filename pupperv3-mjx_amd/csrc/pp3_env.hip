@@ -147,7 +147,11 @@ __device__ __forceinline__ LaneRec<N> fetch_rec(const LaneTab<N>& t, int l) {
 __device__ __forceinline__ int as_i(float f) { return __float_as_int(f); }
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ float dpp_shr4(float v) { return dpp_f<0x114, 0xF>(v, v); }  // lane i <- i-4 (row)
+// lane i <- i-4 (row); lanes 0..3 of a row read 0 (bound_ctrl): every caller selects its own value
+// there, and with no old value to keep the shift is one v_mov_dpp instead of a copy plus the DPP
+__device__ __forceinline__ float dpp_shr4(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, true));
+}
 
 // wave priority by load (env_step_kernel): contact-weight thresholds (contacts of the busier env
 // of the wave, +2 on the leg-leg Newton path) for the upper priority pair / the top priority
@@ -251,6 +255,19 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
     }
   }
   if (l < 12) ang = qj - q0;
+#ifdef PP3_PAD_VALU  // timing diagnostic only: N extra VALU instructions per substep (4 independent chains)
+  {
+    float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f, p3 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < PP3_PAD_VALU / 4; i++)
+      asm volatile("v_add_f32 %0, %0, %0\n v_add_f32 %1, %1, %1\n v_add_f32 %2, %2, %2\n v_add_f32 %3, %3, %3"
+                   : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3));
+  }
+#endif
+#ifdef PP3_PAD_NOP  // timing diagnostic only: N x s_nop 7 (8 issue-stall cycles each) per substep
+#pragma unroll
+  for (int i = 0; i < PP3_PAD_NOP; i++) asm volatile("s_nop 7");
+#endif
   float lq[4] = {1, 0, 0, 0};
   {
     float qloc[4];
@@ -485,11 +502,15 @@ __device__ __forceinline__ bool narrow(const Shared<NC>& s, const TerrainRef& tr
   float p1[3], p2[3];
   {  // robot geoms: world position from LDS; static geoms: from the record (value select)
     const int i1 = rec.s1 >= 0 ? rec.s1 : 0, i2 = rec.s2 >= 0 ? rec.s2 : 0;
+    float l1[3], l2[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { l1[k] = s.gxpos[i1][k]; l2[k] = s.gxpos[i2][k]; }
+    // keep both loads (a pointer select would be a flat load), all six in one LDS round trip
+    asm volatile("" : "+v"(l1[0]), "+v"(l1[1]), "+v"(l1[2]), "+v"(l2[0]), "+v"(l2[1]), "+v"(l2[2]));
+#pragma unroll
     for (int k = 0; k < 3; k++) {
-      float l1 = s.gxpos[i1][k], l2 = s.gxpos[i2][k];
-      asm volatile("" : "+v"(l1), "+v"(l2));  // keep both loads: a pointer select would be a flat load
-      p1[k] = rec.s1 >= 0 ? l1 : rec.p1[k];
-      p2[k] = rec.s2 >= 0 ? l2 : rec.p2[k];
+      p1[k] = rec.s1 >= 0 ? l1[k] : rec.p1[k];
+      p2[k] = rec.s2 >= 0 ? l2[k] : rec.p2[k];
     }
   }
   if (rec.kind == PK_PLANE_SPHERE) {
@@ -1725,15 +1746,20 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     const float gtol = m.gtol_scale * sn;
     // cost and derivatives of the 1-D piecewise quadratic at alpha (alpha is per half)
     auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
-      float t0 = 0, t1 = 0, t2 = 0;
+      // row slot 0 always holds rows (the NFR frictionloss rows come first): its pieces start the
+      // sums instead of being added to zeros
+      static_assert(NFR > 0, "row slot 0 is never empty");
+      float t0, t1, t2;
 #pragma unroll
       for (int t = 0; t < NR; t++) {
-        if (!rowany[t]) continue;
+        if (t > 0 && !rowany[t]) continue;
         const float x = jar[t] + alpha * jv[t];
         const bool lo = x <= thr_lo[t], hi = !lo && x >= thr_hi[t], qd = !lo && !hi;
-        t0 += lo ? clo[t][0] : (hi ? chi[t][0] : cq[t][0]);
-        t1 += lo ? clo[t][1] : (hi ? chi[t][1] : cq[t][1]);
-        t2 += qd ? cq[t][2] : 0.0f;
+        const float p0 = lo ? clo[t][0] : (hi ? chi[t][0] : cq[t][0]);
+        const float p1 = lo ? clo[t][1] : (hi ? chi[t][1] : cq[t][1]);
+        const float p2 = qd ? cq[t][2] : 0.0f;
+        if (t == 0) { t0 = p0; t1 = p1; t2 = p2; }
+        else { t0 += p0; t1 += p1; t2 += p2; }
       }
       t0 = hsum(t0, h) + gauss;
       t1 = hsum(t1, h) + q1;
