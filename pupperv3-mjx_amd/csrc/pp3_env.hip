@@ -185,6 +185,19 @@ __device__ __forceinline__ float hsum(float v, int) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// the same sum, wanted in ONE lane per half (a value the half then stores): after the row
+// butterflies, row_bcast:15 adds row 0's sum into row 1 and row 2's into row 3, so lane 16 of each
+// half (rows 1 and 3) holds R0 + R1 -- the sum hsum leaves there too (fp add commutes) -- without
+// the copy, the wait states and the swap of the full broadcast
+__device__ __forceinline__ float hsum_lane16(float v) {
+  v += dpp_f<0xB1, 0xF>(v, 0.0f);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xF>(v, 0.0f);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xF>(v, 0.0f);  // row_half_mirror
+  v += dpp_f<0x140, 0xF>(v, 0.0f);  // row_mirror
+  // row_bcast:15 -> rows 1, 3; rows 0, 2 are not written (their value is never read)
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x142, 0xA, 0xF, false));
+  return v;
+}
 // this half's bits of a ballot
 __device__ __forceinline__ uint32_t hballot(bool p, int h) {
   const uint64_t m = __ballot(p);
@@ -435,8 +448,8 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
   {  // all ten sums first (independent DPP chains interleave), then the stores
     float t[10];
 #pragma unroll
-    for (int k = 0; k < 10; k++) t[k] = hsum(ci[k], h);
-    if (l == 0)
+    for (int k = 0; k < 10; k++) t[k] = hsum_lane16(ci[k]);
+    if (l == 16)
 #pragma unroll
       for (int k = 0; k < 10; k++) s.crb_base[k] = t[k];
   }
@@ -730,8 +743,8 @@ __device__ __forceinline__ void rne_body_forces(Shared<NC>& s, int l, int h) {
   // all six sums first (independent DPP chains interleave), then the stores
   float t[6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) t[k] = hsum(cf[k], h);
-  if (l == 0)
+  for (int k = 0; k < 6; k++) t[k] = hsum_lane16(cf[k]);
+  if (l == 16)
 #pragma unroll
     for (int k = 0; k < 6; k++) s.cfrc_base[k] = t[k];
 }
