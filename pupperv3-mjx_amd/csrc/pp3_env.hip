@@ -1691,6 +1691,9 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
         for (int c = 0; c < cmax; c++) {
           const bool cv = c < ncon;
           const int sa = __builtin_amdgcn_readlane(lsup, c), sb = __builtin_amdgcn_readlane(lsup, HW + c);
+          // the legs either env's contact c touches, as one scalar bit set (arrowhead path: supports
+          // 0..3 = a leg, 4 = base only): one bit test per leg instead of two compares and an or
+          const uint32_t legs = (1u << (sa & 7)) | (1u << (sb & 7));
           if (cv) {
             const float* G = s.con_G[c];
             const float jn = s.Jc[c][0][dn], j1 = s.Jc[c][1][dn], j2 = s.Jc[c][2][dn];
@@ -1698,10 +1701,10 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
             const float w1 = jn * G[1] + j1 * G[3];
             const float w2 = jn * G[2] + j2 * G[4];
             hess_acc_p<0, 6>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 0 || sb == 0) hess_acc_p<6, 9>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 1 || sb == 1) hess_acc_p<9, 12>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 2 || sb == 2) hess_acc_p<12, 15>(a, s.Jc[c], w0, w1, w2);
-            if (sa == 3 || sb == 3) hess_acc_p<15, 18>(a, s.Jc[c], w0, w1, w2);
+            if (legs & 1u) hess_acc_p<6, 9>(a, s.Jc[c], w0, w1, w2);
+            if (legs & 2u) hess_acc_p<9, 12>(a, s.Jc[c], w0, w1, w2);
+            if (legs & 4u) hess_acc_p<12, 15>(a, s.Jc[c], w0, w1, w2);
+            if (legs & 8u) hess_acc_p<15, 18>(a, s.Jc[c], w0, w1, w2);
           }
         }
         PHASE(14); l = opaque_lane(l);
