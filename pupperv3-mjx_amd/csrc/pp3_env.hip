@@ -868,10 +868,9 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
 #pragma unroll
   for (int st = 0; st < 3; st++) {
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-      col[20 * g + slot] = a[3 * g + st];
-      if (l == 3 * g + st) col[20 * g + 19] = b;  // pivot rhs
-    }
+    for (int g = 0; g < 4; g++) col[20 * g + slot] = a[3 * g + st];
+    // the four pivots' rhs (lane 3 g + st of leg g) in one masked store, not one branch per leg
+    if (l < 12 && l - 3 * (l / 3) == st) col[20 * (l / 3) + 19] = b;
     SYNC();
 #pragma unroll
     for (int g = 0; g < 4; g++) {
@@ -1686,8 +1685,12 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
 #pragma unroll
         for (int j = 0; j < NV; j++) a[j] = mrow[j];
         const float dD = s.dofD[dn];
+        // the diagonal D on this lane's own column: a[j] + dD * [j == lp] as one fma per column
+        // (dD >= 0, so the other columns add +0 exactly as a + 0.0f did), the 0/1 factor from a
+        // bit field -- no per-column VCC compare and the wait states a v_cndmask needs after it
+        const uint32_t onehot = 1u << lp;
 #pragma unroll
-        for (int j = 0; j < NV; j++) a[j] += (j == lp) ? dD : 0.0f;
+        for (int j = 0; j < NV; j++) a[j] = fmaf(dD, (float)((onehot >> j) & 1u), a[j]);
         for (int c = 0; c < cmax; c++) {
           const bool cv = c < ncon;
           const int sa = __builtin_amdgcn_readlane(lsup, c), sb = __builtin_amdgcn_readlane(lsup, HW + c);
