@@ -1580,14 +1580,14 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       const float x2 = d2 - ar[t];
       xws[t] = x1;
       xsm[t] = x2;
-      if (isfr[t]) {
-        const float rf = Rr[t] * fl[t];
-        cws += (x1 <= -rf) ? (-fl[t] * x1 - 0.5f * rf * fl[t]) : (x1 >= rf) ? (fl[t] * x1 - 0.5f * rf * fl[t]) : 0.5f * Dr[t] * x1 * x1;
-        csm += (x2 <= -rf) ? (-fl[t] * x2 - 0.5f * rf * fl[t]) : (x2 >= rf) ? (fl[t] * x2 - 0.5f * rf * fl[t]) : 0.5f * Dr[t] * x2 * x2;
-      } else {
-        cws += (x1 < 0) ? 0.5f * Dr[t] * x1 * x1 : 0.0f;
-        csm += (x2 < 0) ? 0.5f * Dr[t] * x2 * x2 : 0.0f;
-      }
+      // both row kinds' costs as selects (a wave holds both kinds, so both were executed anyway,
+      // behind exec-mask branches)
+      const float rf = Rr[t] * fl[t];
+      const float q1 = 0.5f * Dr[t] * x1 * x1, q2 = 0.5f * Dr[t] * x2 * x2;
+      const float f1 = (x1 <= -rf) ? (-fl[t] * x1 - 0.5f * rf * fl[t]) : (x1 >= rf) ? (fl[t] * x1 - 0.5f * rf * fl[t]) : q1;
+      const float f2 = (x2 <= -rf) ? (-fl[t] * x2 - 0.5f * rf * fl[t]) : (x2 >= rf) ? (fl[t] * x2 - 0.5f * rf * fl[t]) : q2;
+      cws += isfr[t] ? f1 : ((x1 < 0) ? q1 : 0.0f);
+      csm += isfr[t] ? f2 : ((x2 < 0) ? q2 : 0.0f);
     }
     if (l < NV) {  // lane l: dof dn = pnat(l), the row it holds in mrow
       const int dn = pnat(l);
@@ -1620,16 +1620,15 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       const int r = l + HW * t;
       const float x = iter > 0 ? row_dot(s, r, nl, ncon, s.qacc) - ar[t] : (use_smooth ? xsm[t] : xws[t]);
       jar[t] = x;
-      float f, Dq = 0.0f;
-      if (isfr[t]) {
-        const float rf = Rr[t] * fl[t];
-        if (x <= -rf) f = fl[t];
-        else if (x >= rf) f = -fl[t];
-        else { f = -Dr[t] * x; Dq = Dr[t]; }
-      } else {
-        if (x >= 0) f = 0;
-        else { f = -Dr[t] * x; Dq = Dr[t]; }
-      }
+      // constraint state and force, as selects (the nested branches cost more exec-mask scalar
+      // instructions than the few selects): frictionloss rows linear below -R f / above +R f,
+      // quadratic between; contact and limit rows zero when x >= 0, quadratic below
+      const float rf = Rr[t] * fl[t];
+      const float fq = -Dr[t] * x;
+      const bool lo = isfr[t] && x <= -rf;
+      const bool hi = !lo && (isfr[t] ? x >= rf : x >= 0);
+      const float f = lo ? fl[t] : (hi ? (isfr[t] ? -fl[t] : 0.0f) : fq);
+      const float Dq = (lo || hi) ? 0.0f : Dr[t];
       s.efc_force[r] = f;
       s.efc_D[r] = Dq;  // active D (0 when not quadratic) for the Hessian
     }
