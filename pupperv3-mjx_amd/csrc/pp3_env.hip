@@ -864,7 +864,11 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
   l = opaque_lane(l);
   const int slot = l < NV ? l : NV;
   const int lp = l < NV ? l : NV - 1;
-  float dinv = 1.0f;
+  // lane p < 12 is the pivot of leg p / 3 in round p % 3; its 1/D is the reciprocal of the value
+  // it publishes then (its own diagonal), read back with that round's pivot columns: one select
+  // per round instead of a compare and select per pivot (12 per call)
+  const int pg = lp < 12 ? lp / 3 : 0, pst = lp < 12 ? lp - 3 * pg : 3;
+  float mydiag = 1.0f;
 #pragma unroll
   for (int st = 0; st < 3; st++) {
 #pragma unroll
@@ -872,6 +876,10 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
     // the four pivots' rhs (lane 3 g + st of leg g) in one masked store, not one branch per leg
     if (l < 12 && l - 3 * (l / 3) == st) col[20 * (l / 3) + 19] = b;
     SYNC();
+    {
+      const float pv = col[20 * pg + slot];
+      mydiag = (pst == st) ? pv : mydiag;
+    }
 #pragma unroll
     for (int g = 0; g < 4; g++) {
       const int k = 3 * g + st;
@@ -893,8 +901,8 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
         const float4 v = *reinterpret_cast<const float4*>(c + q);
         r[q] = v.x; r[q + 1] = v.y; r[q + 2] = v.z; r[q + 3] = v.w;
       }
-      const float ik = frcp(fmaxf(r[k], MINVAL));
-      dinv = (l == k) ? ik : dinv;
+      float ik = frcp(fmaxf(r[k], MINVAL));
+      PIN("+v"(ik));  // (on every lane: otherwise the pivot read and rcp sink into a branch on l > k)
       const float lik = (l > k) ? a[k] * ik : 0.0f;  // zero on rows above the pivot and other legs
 #pragma unroll
       for (int jj = 0; jj < 3; ++jj)
@@ -949,7 +957,8 @@ __device__ __forceinline__ float ldl_arrow_solve(float (&a)[NV], float b, int l,
 #pragma unroll
     for (int i = 5; i > c; --i) y[c] = y[c] - S[i][c] * y[i];
   // leg rows: U x = y from registers (base part) and the rows below in the same leg (DPP)
-  const int li = lp < 12 ? lp - 3 * (lp / 3) : 3;  // level in the leg (3 = base row)
+  const float dinv = frcp(fmaxf(mydiag, MINVAL));  // the pivot's ik (base and dummy lanes: rcp(1) = 1)
+  const int li = pst;  // level in the leg (3 = base row)
   float t = b;
 #pragma unroll
   for (int c = 0; c < 6; c++) t -= a[12 + c] * y[c];
