@@ -1449,14 +1449,29 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   // ---- phase 4: M entries, RNE body forces, contact Jacobians ----
   const LaneRec<3> rm = rm_pf;  // (prefetched at the substep start; also read by phases 13 and 7)
   
+  // every M pair's twelve operands in one LDS round (pinned; lanes without a pair read row 0):
+  // otherwise each pair waits for its own loads, behind the previous pair's stores
+  constexpr int NT = (NMPAIR + HW - 1) / HW;  // compile-time trip count
+  float cd[NT][6], fi[NT][6];
 #pragma unroll
-  for (int t = 0; t < (NMPAIR + HW - 1) / HW; t++) {  // compile-time trip count
+  for (int t = 0; t < NT; t++) {
+    const int ij = as_i(rm.f[LM_IJ + t]);
+    const int i = ij < 0 ? 0 : (ij & 0xff), j = ij < 0 ? 0 : (ij >> 8);
+#pragma unroll
+    for (int k = 0; k < 6; k++) { cd[t][k] = s.cdof[j][k]; fi[t][k] = s.x.a.F[i][k]; }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; t++)
+    PIN("+v"(cd[t][0]), "+v"(cd[t][1]), "+v"(cd[t][2]), "+v"(cd[t][3]), "+v"(cd[t][4]), "+v"(cd[t][5]),
+        "+v"(fi[t][0]), "+v"(fi[t][1]), "+v"(fi[t][2]), "+v"(fi[t][3]), "+v"(fi[t][4]), "+v"(fi[t][5]));
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
     const int ij = as_i(rm.f[LM_IJ + t]);
     if (ij < 0) continue;
     const int i = ij & 0xff, j = ij >> 8;
     float v = 0;
 #pragma unroll
-    for (int k = 0; k < 6; k++) v += s.cdof[j][k] * s.x.a.F[i][k];
+    for (int k = 0; k < 6; k++) v += cd[t][k] * fi[t][k];
     v += rm.f[LM_ARM + t];  // armature on the diagonal, 0 elsewhere
     s.M[i][j] = v;
     s.M[j][i] = v;
