@@ -704,14 +704,26 @@ __device__ __forceinline__ void rne_chain(Shared<NC>& s, const DevModel& m, int 
   // free joint in closed form: its translational cdof are the unit vectors (com_pos), so the
   // velocity after them is (0, v); each rotational dof's cdof_dot = (0, v) x cdof = (0, v x a_d),
   // hence cacc = (0, -g + v x w) with w = sum_d a_d qvel[3+d], and cvel = (w, v + sum_d b_d qvel[3+d])
+  // (the base's three rotational cdof rows and six velocities in one pinned LDS round)
+  float bcd[3][6], bq[6];
+#pragma unroll
+  for (int d = 0; d < 3; d++)
+#pragma unroll
+    for (int k = 0; k < 6; k++) bcd[d][k] = s.cdof[3 + d][k];
+#pragma unroll
+  for (int k = 0; k < 6; k++) bq[k] = s.qvel[k];
+  PIN("+v"(bcd[0][0]), "+v"(bcd[0][1]), "+v"(bcd[0][2]), "+v"(bcd[0][3]), "+v"(bcd[0][4]), "+v"(bcd[0][5]),
+      "+v"(bcd[1][0]), "+v"(bcd[1][1]), "+v"(bcd[1][2]), "+v"(bcd[1][3]), "+v"(bcd[1][4]), "+v"(bcd[1][5]),
+      "+v"(bcd[2][0]), "+v"(bcd[2][1]), "+v"(bcd[2][2]), "+v"(bcd[2][3]), "+v"(bcd[2][4]), "+v"(bcd[2][5]),
+      "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(bq[4]), "+v"(bq[5]));
   float w[3] = {0, 0, 0}, bsum[3] = {0, 0, 0};
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    const float q = s.qvel[3 + d];
+    const float q = bq[3 + d];
 #pragma unroll
-    for (int k = 0; k < 3; k++) { w[k] += s.cdof[3 + d][k] * q; bsum[k] += s.cdof[3 + d][3 + k] * q; }
+    for (int k = 0; k < 3; k++) { w[k] += bcd[d][k] * q; bsum[k] += bcd[d][3 + k] * q; }
   }
-  const float v0 = s.qvel[0], v1 = s.qvel[1], v2 = s.qvel[2];
+  const float v0 = bq[0], v1 = bq[1], v2 = bq[2];
   float cv[6] = {w[0], w[1], w[2], v0 + bsum[0], v1 + bsum[1], v2 + bsum[2]};
   float ca[6] = {0, 0, 0, -m.gravity[0] + (v1 * w[2] - v2 * w[1]), -m.gravity[1] + (v2 * w[0] - v0 * w[2]),
                  -m.gravity[2] + (v0 * w[1] - v1 * w[0])};
@@ -758,17 +770,25 @@ __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m,
   const bool base = l < 6;
   const int b = base ? 2 : l - 4, last = 2 + 3 * ((b - 2) / 3) + 2;  // dof 6+3g+k <-> body 2+3g+k
   const float* r0 = base ? s.crb_base : s.cinert[b];
-  float crb[10];
+  // every operand (36 words) in one pinned LDS round: unpinned, the compiler reused one register
+  // pair for the links' rows and waited after each pair of words
+  const int b1 = b + 1 <= last ? b + 1 : b, b2 = b + 2 <= last ? b + 2 : b;
+  float crb[10], c1[10], c2[10], cdv[6];
 #pragma unroll
-  for (int k = 0; k < 10; k++) crb[k] = r0[k];
+  for (int k = 0; k < 10; k++) { crb[k] = r0[k]; c1[k] = s.cinert[b1][k]; c2[k] = s.cinert[b2][k]; }
 #pragma unroll
-  for (int o = 1; o < 3; o++) {
-    const int bb = b + o <= last ? b + o : b;
-    const float w = (!base && b + o <= last) ? 1.0f : 0.0f;
+  for (int k = 0; k < 6; k++) cdv[k] = s.cdof[l][k];
+  PIN("+v"(crb[0]), "+v"(crb[1]), "+v"(crb[2]), "+v"(crb[3]), "+v"(crb[4]), "+v"(crb[5]), "+v"(crb[6]), "+v"(crb[7]),
+      "+v"(crb[8]), "+v"(crb[9]), "+v"(cdv[0]), "+v"(cdv[1]), "+v"(cdv[2]), "+v"(cdv[3]), "+v"(cdv[4]), "+v"(cdv[5]));
+  PIN("+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]), "+v"(c1[4]), "+v"(c1[5]), "+v"(c1[6]), "+v"(c1[7]),
+      "+v"(c1[8]), "+v"(c1[9]), "+v"(c2[0]), "+v"(c2[1]), "+v"(c2[2]), "+v"(c2[3]), "+v"(c2[4]), "+v"(c2[5]),
+      "+v"(c2[6]), "+v"(c2[7]), "+v"(c2[8]), "+v"(c2[9]));
+  const float w1 = (!base && b + 1 <= last) ? 1.0f : 0.0f, w2 = (!base && b + 2 <= last) ? 1.0f : 0.0f;
 #pragma unroll
-    for (int k = 0; k < 10; k++) crb[k] += w * s.cinert[bb][k];
-  }
-  mul_inert_vec(s.x.a.F[l], crb, s.cdof[l]);
+  for (int k = 0; k < 10; k++) crb[k] += w1 * c1[k];
+#pragma unroll
+  for (int k = 0; k < 10; k++) crb[k] += w2 * c2[k];
+  mul_inert_vec(s.x.a.F[l], crb, cdv);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1396,6 +1416,16 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   }
   {
     const LaneRec<7> rl = fetch_rec(m.lane_lim, l);
+    // every LDS operand of the phase in one pinned round, indices clamped on the lanes that do
+    // not use them (read inside the lane branches below, each was a round trip of its own)
+    const int jlim = l < 2 * (NJ - 1) ? 1 + (l >> 1) : 1;
+    const bool actl = l < NU;
+    const int adof = actl ? as_i(rl.f[LL_ACT_DOF]) : 0, aqadr = actl ? as_i(rl.f[LL_ACT_QADR]) : 0;
+    float lq = s.qpos[7 + jlim - 1], lqv = s.qvel[6 + jlim - 1], fqv = s.qvel[6 + (l < NFR ? l : 0)];
+    float actrl = s.ctrl[actl ? l : 0], aq = s.qpos[aqadr], aqv = s.qvel[adof];
+    float skp = s.kp, skd = s.kd;
+    int sdr = s.dr_on;
+    PIN("+v"(lq), "+v"(lqv), "+v"(fqv), "+v"(actrl), "+v"(aq), "+v"(aqv), "+v"(skp), "+v"(skd), "+v"(sdr));
     // joint limits: lane = 2*(j-1) + side_hi, rows ordered like the oracle (mj_instantiateLimit)
     bool act = false;
     float value = 0;
@@ -1404,7 +1434,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       j = 1 + (l >> 1);
       const float side = (l & 1) ? 1.0f : -1.0f;
       if (as_i(rl.f[LL_LIM_ON])) {
-        value = side * (rl.f[LL_RANGE] - s.qpos[7 + j - 1]);
+        value = side * (rl.f[LL_RANGE] - lq);
         act = value < rl.f[LL_MARGIN];
       }
     }
@@ -1420,23 +1450,25 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       const int r = NFR + slot;
       s.efc_R[r] = R;
       s.efc_D[r] = 1.0f / R;
-      s.efc_aref[r] = -rl.f[LL_B] * (sg * s.qvel[dof]) - rl.f[LL_K] * imp * (value - rl.f[LL_MARGIN]);
+      s.efc_aref[r] = -rl.f[LL_B] * (sg * lqv) - rl.f[LL_K] * imp * (value - rl.f[LL_MARGIN]);
+      (void)dof;
     }
     if (l == 0) s.nl = __popc(mask) < NLMAX ? __popc(mask) : NLMAX;
     if (l < NFR) {  // dof frictionloss rows (R, b precomputed: pos = 0)
       const int dof = 6 + l;
       s.efc_R[l] = rl.f[LL_FR_R];
       s.efc_D[l] = 1.0f / rl.f[LL_FR_R];
-      s.efc_aref[l] = -rl.f[LL_FR_B] * s.qvel[dof];
+      s.efc_aref[l] = -rl.f[LL_FR_B] * fqv;
+      (void)dof;
     }
     if (l < NU) {  // actuation (affine PD + force clamp)
-      const int d = as_i(rl.f[LL_ACT_DOF]), flags = as_i(rl.f[LL_ACT_FLAGS]);
-      float ctrl = s.ctrl[l];
+      const int d = adof, flags = as_i(rl.f[LL_ACT_FLAGS]);
+      float ctrl = actrl;
       if (flags & ACTF_CTRLLIMITED) ctrl = fminf(fmaxf(ctrl, rl.f[LL_CRANGE]), rl.f[LL_CRANGE + 1]);
       const float gear = rl.f[LL_GEAR];
-      const float len = gear * s.qpos[as_i(rl.f[LL_ACT_QADR])], vel = gear * s.qvel[d];
+      const float len = gear * aq, vel = gear * aqv;
       float gain = rl.f[LL_GAIN], b0 = rl.f[LL_BIAS], b1 = rl.f[LL_BIAS + 1], b2 = rl.f[LL_BIAS + 2];
-      if (s.dr_on) { gain = s.kp; b1 = -s.kp; b2 = -s.kd; }
+      if (sdr) { gain = skp; b1 = -skp; b2 = -skd; }
       float force = gain * ctrl;
       if (flags & ACTF_AFFINE) force += b0 + b1 * len + b2 * vel;
       if (flags & ACTF_FORCELIMITED) force = fminf(fmaxf(force, rl.f[LL_FRANGE]), rl.f[LL_FRANGE + 1]);
@@ -1509,25 +1541,40 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   // ---- phase 5: qfrc_bias/smooth (subtree sums of body forces), contact edge rows ----
   {
   if (l < NV) {
+    // base dofs: the whole tree's cfrc; a leg link: itself + the (<= 2) links below (cacc holds
+    // cfrc now; dof 6+3g+k <-> body 2+3g+k, checked at create).  Every operand (32 words) in one
+    // pinned LDS round, the base/leg choice a select: unpinned, the links' rows and the cdof row
+    // were loaded a register pair at a time, each waited for
+    const bool base = l < 6;
+    const int b = base ? 2 : l - 4, last = 2 + 3 * ((b - 2) / 3) + 2;
+    const int b1 = b + 1 <= last ? b + 1 : b, b2 = b + 2 <= last ? b + 2 : b;
+    float r0[6], c0[6], c1[6], c2[6], cdv[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      r0[k] = s.cfrc_base[k];
+      c0[k] = s.x.a.cacc[b][k];
+      c1[k] = s.x.a.cacc[b1][k];
+      c2[k] = s.x.a.cacc[b2][k];
+      cdv[k] = s.cdof[l][k];
+    }
+    float qv = s.qvel[l], qa = s.qfrc_act[l];
+    PIN("+v"(r0[0]), "+v"(r0[1]), "+v"(r0[2]), "+v"(r0[3]), "+v"(r0[4]), "+v"(r0[5]), "+v"(c0[0]), "+v"(c0[1]),
+        "+v"(c0[2]), "+v"(c0[3]), "+v"(c0[4]), "+v"(c0[5]), "+v"(cdv[0]), "+v"(cdv[1]), "+v"(cdv[2]), "+v"(cdv[3]),
+        "+v"(cdv[4]), "+v"(cdv[5]), "+v"(qv), "+v"(qa));
+    PIN("+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]), "+v"(c1[4]), "+v"(c1[5]), "+v"(c2[0]), "+v"(c2[1]),
+        "+v"(c2[2]), "+v"(c2[3]), "+v"(c2[4]), "+v"(c2[5]));
+    const float w1 = b + 1 <= last ? 1.0f : 0.0f, w2 = b + 2 <= last ? 1.0f : 0.0f;
     float cf[6];
-    if (l < 6) {
 #pragma unroll
-      for (int k = 0; k < 6; k++) cf[k] = s.cfrc_base[k];
-    } else {  // subtree of a leg link: itself + the (<= 2) links below (cacc holds cfrc now)
-      const int b = l - 4, last = 2 + 3 * ((b - 2) / 3) + 2;  // dof 6+3g+k <-> body 2+3g+k (checked at create)
-#pragma unroll
-      for (int k = 0; k < 6; k++) cf[k] = s.x.a.cacc[b][k];
-#pragma unroll
-      for (int o = 1; o < 3; o++) {
-        const int bb = b + o <= last ? b + o : b;
-        const float w = b + o <= last ? 1.0f : 0.0f;
-#pragma unroll
-        for (int k = 0; k < 6; k++) cf[k] += w * s.x.a.cacc[bb][k];
-      }
+    for (int k = 0; k < 6; k++) {
+      float t = c0[k];
+      t += w1 * c1[k];
+      t += w2 * c2[k];
+      cf[k] = base ? r0[k] : t;
     }
     float bias = 0;
-    for (int k = 0; k < 6; k++) bias += s.cdof[l][k] * cf[k];
-    s.qfrc_smooth[l] = -rm.f[LM_DAMP] * s.qvel[l] - bias + s.qfrc_act[l];
+    for (int k = 0; k < 6; k++) bias += cdv[k] * cf[k];
+    s.qfrc_smooth[l] = -rm.f[LM_DAMP] * qv - bias + qa;
   }
   }
   const int nl = s.nl;
