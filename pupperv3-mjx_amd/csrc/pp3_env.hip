@@ -2626,30 +2626,44 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   const float cn = sqrtf(cmd0 * cmd0 + cmd1 * cmd1 + cmd2 * cmd2);
   float r_torq = 0, r_jacc = 0, r_mech = 0, r_arate = 0, r_stand = 0, r_standv = 0, r_abd = 0;
   float r_air = 0, r_slip = 0, r_knee = 0, r_body = 0;
-  if (l < NV) r_torq = s.qfrc_act[l] * s.qfrc_act[l];
+  // every per-lane LDS operand of the terms below in one pinned round (indices clamped on the
+  // lanes that do not use them); read inside the lane branches they were round trips of their own
+  const int l18 = l < NV ? l : 0, l12 = l < 12 ? l : 0, l4 = l < 4 ? l : 0, lc = l < NC ? l : 0;
+  const int bleg = l < 4 ? as_i(re.f[LE_LEG]) : 1;
+  float fa = s.qfrc_act[l18], fa6 = s.qfrc_act[6 + l12], qv = s.qvel[6 + l12], qp = s.qpos[7 + l12];
+  float lvel = s.st[PP3_S_LAST_VEL + l12], lact = s.st[PP3_S_LAST_ACT + l12];
+  float airt = s.st[PP3_S_AIR_TIME + l4], fst = s.x.e.first[l4];
+  float sp[3], xb[3], xdab[3], xdvb[2];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { sp[k] = s.foot_xpos[l4][k]; xb[k] = s.xpos[bleg][k]; xdab[k] = s.x.e.xda[bleg][k]; }
+  xdvb[0] = s.x.e.xdv[bleg][0];
+  xdvb[1] = s.x.e.xdv[bleg][1];
+  int fcm = s.x.e.filt_cm[l4], ncon_r = s.ncon, cpair = s.con_pair[lc];
+  float cdist = s.con_dist[lc];
+  PIN("+v"(fa), "+v"(fa6), "+v"(qv), "+v"(qp), "+v"(lvel), "+v"(lact), "+v"(airt), "+v"(fst), "+v"(sp[0]), "+v"(sp[1]),
+      "+v"(sp[2]), "+v"(xb[0]), "+v"(xb[1]), "+v"(xb[2]), "+v"(xdab[0]), "+v"(xdab[1]), "+v"(xdab[2]), "+v"(xdvb[0]),
+      "+v"(xdvb[1]), "+v"(fcm), "+v"(ncon_r), "+v"(cpair), "+v"(cdist));
+  if (l < NV) r_torq = fa * fa;
   if (l < 12) {
-    const float qv = s.qvel[6 + l], qp = s.qpos[7 + l];
-    const float acc = (qv - s.st[PP3_S_LAST_VEL + l]) / m.env_dt;
+    const float acc = (qv - lvel) / m.env_dt;
     r_jacc = acc * acc;
-    r_mech = fabsf(s.qfrc_act[6 + l] * qv);
-    const float da = act_in - s.st[PP3_S_LAST_ACT + l];  // act_in = action[l] (prologue load)
+    r_mech = fabsf(fa6 * qv);
+    const float da = act_in - lact;  // act_in = action[l] (prologue load)
     r_arate = da * da;
     r_stand = fabsf(qp - re.f[LE_POSE]);
     r_standv = fabsf(qv);
     if (l % 3 == 1) { const float t = qp - re.f[LE_ABD]; r_abd = t * t; }
   }
   if (l < 4) {
-    r_air = (s.st[PP3_S_AIR_TIME + l] - 0.1f) * s.x.e.first[l];
-    const int b = as_i(re.f[LE_LEG]);
-    const float* sp = s.foot_xpos[l];
-    const float off[3] = {sp[0] - s.xpos[b][0], sp[1] - s.xpos[b][1], sp[2] - s.xpos[b][2]};
+    r_air = (airt - 0.1f) * fst;
+    const float off[3] = {sp[0] - xb[0], sp[1] - xb[1], sp[2] - xb[2]};
     float cr[3];
-    cross3(cr, s.x.e.xda[b], off);
-    const float vx = s.x.e.xdv[b][0] + cr[0], vy = s.x.e.xdv[b][1] + cr[1];
-    r_slip = (vx * vx + vy * vy) * (s.x.e.filt_cm[l] ? 1.0f : 0.0f);
+    cross3(cr, xdab, off);
+    const float vx = xdvb[0] + cr[0], vy = xdvb[1] + cr[1];
+    r_slip = (vx * vx + vy * vy) * (fcm ? 1.0f : 0.0f);
   }
-  if (l < s.ncon && s.con_dist[l] < 0.0f) {  // geom_collision: (contact, id) matches with dist < 0
-    const v4f kb = reinterpret_cast<const v4f*>(&m.pair_con[s.con_pair[l]])[3];  // knee, body counts (host)
+  if (l < ncon_r && cdist < 0.0f) {  // geom_collision: (contact, id) matches with dist < 0
+    const v4f kb = reinterpret_cast<const v4f*>(&m.pair_con[cpair])[3];  // knee, body counts (host)
     r_knee = kb[1];
     r_body = kb[2];
   }
