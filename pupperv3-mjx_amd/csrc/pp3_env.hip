@@ -458,11 +458,19 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
   if (geom || foot) {
     const int b = as_i(rc.f[LC_PT_BODY]);
     const float lp[3] = {rc.f[LC_PT_POS], rc.f[LC_PT_POS + 1], rc.f[LC_PT_POS + 2]};
+    // the body's frame in one pinned round (the stores below may alias it for the compiler, which
+    // otherwise re-reads each position word after the previous store)
+    float q[4], xb[3];
+#pragma unroll
+    for (int k = 0; k < 4; k++) q[k] = s.xquat[b][k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) xb[k] = s.xpos[b][k];
+    PIN("+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(xb[0]), "+v"(xb[1]), "+v"(xb[2]));
     float R[9], off[3];
-    quat2mat(s.xquat[b], R);
+    quat2mat(q, R);
     matvec(off, R, lp);
     float* dst = geom ? s.gxpos[l] : s.foot_xpos[l - 16];
-    for (int k = 0; k < 3; k++) dst[k] = s.xpos[b][k] + off[k];
+    for (int k = 0; k < 3; k++) dst[k] = xb[k] + off[k];
   }
 }
 
