@@ -2602,35 +2602,50 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   SYNC();
   PHASE(11);
   // ---- brax x/xd (lanes 1..13), feet (16..19) ----
+  // every LDS operand of x/xd, the feet, done and the command in one pinned round (indices
+  // clamped on the lanes that do not use them; none of them is written before its use below)
+  const int tb = m.torso_body;
+  const int bx = (l >= 1 && l < NB) ? l : 1, fx = (l >= 16 && l < 20) ? l - 16 : 0;
+  float xbb[3], cm[3], cv[6], qt[4];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { xbb[k] = s.xpos[bx][k]; cm[k] = s.com[k]; }
+#pragma unroll
+  for (int k = 0; k < 6; k++) cv[k] = s.cvel[bx][k];
+#pragma unroll
+  for (int k = 0; k < 4; k++) qt[k] = s.xquat[tb][k];
+  float fz = s.foot_xpos[fx][2], lcst = s.st[PP3_S_LAST_CONTACT + fx], airt0 = s.st[PP3_S_AIR_TIME + fx];
+  float xtz = s.xpos[tb][2], qpl = s.qpos[7 + (l < 12 ? l : 0)];
+  float cmd0 = s.st[PP3_S_COMMAND], cmd1 = s.st[PP3_S_COMMAND + 1], cmd2 = s.st[PP3_S_COMMAND + 2];
+  PIN("+v"(xbb[0]), "+v"(xbb[1]), "+v"(xbb[2]), "+v"(cm[0]), "+v"(cm[1]), "+v"(cm[2]), "+v"(cv[0]), "+v"(cv[1]),
+      "+v"(cv[2]), "+v"(cv[3]), "+v"(cv[4]), "+v"(cv[5]), "+v"(qt[0]), "+v"(qt[1]), "+v"(qt[2]), "+v"(qt[3]));
+  PIN("+v"(fz), "+v"(lcst), "+v"(airt0), "+v"(xtz), "+v"(qpl), "+v"(cmd0), "+v"(cmd1), "+v"(cmd2));
   if (l >= 1 && l < NB) {
     const int b = l;
-    const float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]};
+    const float off[3] = {xbb[0] - cm[0], xbb[1] - cm[1], xbb[2] - cm[2]};
     float cr[3];
-    cross3(cr, s.cvel[b], off);
-    for (int k = 0; k < 3; k++) { s.x.e.xdv[b][k] = s.cvel[b][3 + k] + cr[k]; s.x.e.xda[b][k] = s.cvel[b][k]; }
+    cross3(cr, cv, off);
+    for (int k = 0; k < 3; k++) { s.x.e.xdv[b][k] = cv[3 + k] + cr[k]; s.x.e.xda[b][k] = cv[k]; }
   }
   if (l >= 16 && l < 20) {
     const int f = l - 16;
-    const float cz = s.foot_xpos[f][2] - m.foot_radius;
-    const int last = s.st[PP3_S_LAST_CONTACT + f] != 0.0f;
+    const float cz = fz - m.foot_radius;
+    const int last = lcst != 0.0f;
     const int c = cz < 1e-3f;
     s.x.e.contact[f] = c;
     s.x.e.filt_mm[f] = c | last;
     s.x.e.filt_cm[f] = (cz < 3e-2f) | last;
-    s.x.e.first[f] = (s.st[PP3_S_AIR_TIME + f] > 0.0f && (c | last)) ? 1.0f : 0.0f;
-    s.st[PP3_S_AIR_TIME + f] += m.dt;
+    s.x.e.first[f] = (airt0 > 0.0f && (c | last)) ? 1.0f : 0.0f;
+    s.st[PP3_S_AIR_TIME + f] = airt0 + m.dt;
   }
   SYNC();
   // ---- done (environment.py:383-388): tilt and height on every lane, joint limits on 0..11 ----
-  const int tb = m.torso_body;
   const float z0[3] = {0, 0, 1};
   float ru_t[3];
-  b_rotate(ru_t, z0, s.xquat[tb]);
-  const bool jviol = l < 12 && (s.qpos[7 + l] < re.f[LE_JLO] || s.qpos[7 + l] > re.f[LE_JHI]);
-  const bool isdone = hballot(jviol, h) != 0 || ru_t[2] < m.cos_term_angle || s.xpos[tb][2] < m.term_z;
+  b_rotate(ru_t, z0, qt);
+  const bool jviol = l < 12 && (qpl < re.f[LE_JLO] || qpl > re.f[LE_JHI]);
+  const bool isdone = hballot(jviol, h) != 0 || ru_t[2] < m.cos_term_angle || xtz < m.term_z;
   // ---- rewards (rewards.py) ----
   // sums over joints / dofs / feet / contacts: one element per lane, then a half-wave sum
-  const float cmd0 = s.st[PP3_S_COMMAND], cmd1 = s.st[PP3_S_COMMAND + 1], cmd2 = s.st[PP3_S_COMMAND + 2];
   const float cn = sqrtf(cmd0 * cmd0 + cmd1 * cmd1 + cmd2 * cmd2);
   float r_torq = 0, r_jacc = 0, r_mech = 0, r_arate = 0, r_stand = 0, r_standv = 0, r_abd = 0;
   float r_air = 0, r_slip = 0, r_knee = 0, r_body = 0;
