@@ -93,7 +93,8 @@ def one_step_err(env, n_sample=256, seed=0, dr_table=None, terrain=None, auto_re
     restatement from IDENTICAL states, on the workload's own states after the timed run.  Each
     sampled env is checked against an oracle env built on ITS model: its domain-randomisation row
     (`dr_table`) and its terrain (`terrain`).  With auto-reset on, envs that ended their episode in
-    this step hold the episode's first state, not a physics step: they are left out (counted)."""
+    this step hold the episode's first state, not a physics step: they are left out (counted).
+    Returns (one_step_err, ls_cap): ls_cap = ls_cap_stats on the same states and actions."""
     import numpy as np
     from pupperv3_mjx import _abi, _lib
     from oracle import oracle as O
@@ -131,13 +132,84 @@ def one_step_err(env, n_sample=256, seed=0, dr_table=None, terrain=None, auto_re
         return {"max": float(x.max()), "median": float(np.median(x)), "p99": float(np.percentile(x, 99))}
 
     ok = ~flagged
-    return {"envs": int(len(ids)), "substeps": int(env._n_frames), "vs": "fp64 oracle restatement, identical start state",
-            "qpos_abs": st(dq), "qvel_abs": st(dv), "qpos_rel": st(rq),
-            "constraint_flip_envs": int(flagged.sum()),
-            "per_env_model": {"dr": dr_table is not None, "terrain": terrain is not None},
-            "auto_reset_envs_excluded": n_reset,
-            "qpos_abs_max_unflagged": float(dq[ok].max()) if ok.any() else None,
-            "qvel_abs_max_unflagged": float(dv[ok].max()) if ok.any() else None}
+    err = {"envs": int(len(ids)), "substeps": int(env._n_frames), "vs": "fp64 oracle restatement, identical start state",
+           "qpos_abs": st(dq), "qvel_abs": st(dv), "qpos_rel": st(rq),
+           "constraint_flip_envs": int(flagged.sum()),
+           "per_env_model": {"dr": dr_table is not None, "terrain": terrain is not None},
+           "auto_reset_envs_excluded": n_reset,
+           "qpos_abs_max_unflagged": float(dq[ok].max()) if ok.any() else None,
+           "qvel_abs_max_unflagged": float(dv[ok].max()) if ok.any() else None}
+    return err, ls_cap_stats(env, rec0[ids], obs0[ids], a[ids], ids, dr_table, terrain)
+
+
+def ls_cap_stats(env, recs, obs, acts, ids, dr_table=None, terrain=None, converged_iters=50):
+    """How much of the hot path rests on the unpinned truncated line search (verdict r04 item 1).
+    The model runs Newton with iterations=1, ls_iterations=5 (test_pupper_model.xml:57): every
+    substep's qacc is ONE line-searched Newton step.  Where the search ends by its 5-evaluation cap
+    instead of by convergence, the returned alpha comes from PrimalSearch's exit rule, which MuJoCo's
+    documentation does not specify (the oracle and the kernel restate it identically).  On the given
+    post-window states (the same states and actions as one_step_err), one env step of the oracle is
+    replayed (a) as the reference runs it, counting how each Newton search ended, in fp64 and in fp32
+    (the kernel's arithmetic, same exit rule), and (b) in fp64 with the search run to convergence
+    (ls_iterations = `converged_iters`) from the identical state: the (a)-(b) one-step qpos / qvel
+    differences bound what the undocumented exit rule can move."""
+    import numpy as np
+    from oracle import oracle as O
+    cfg = env.config_struct
+
+    def model_of(i, iters):
+        m = env.sys_model.struct if terrain is None else O.model_with_terrain(env.sys_model.struct, terrain[i])
+        return O.with_ls_iterations(m, iters) if iters else m
+
+    counts = {p: {"searches": 0, "evals": 0, "converged": 0, "capped": 0, "stalled": 0} for p in ("f64", "f32")}
+    counts["f64_converged_run"] = {"searches": 0, "capped": 0, "stalled": 0}
+    capped_env = []
+    dq, dv, rq = [], [], []
+    cap_iters = int(env.sys_model.struct.ls_iterations)
+    for p in ("f64", "f32"):
+        O.ls_take(p)
+    for j, i in enumerate(ids):
+        dr = None if dr_table is None else dr_table[i]
+        s0 = dict(state=_oracle_record(recs[j]), obs=obs[j].astype(np.float64))
+        act = acts[j].astype(np.float64)
+        outs = {}
+        for p in ("f64", "f32"):
+            o = O.OracleEnv(model_of(i, 0), cfg, dr=dr, precision=p).step(s0, act)
+            c = O.ls_take(p)
+            for k in counts[p]:
+                counts[p][k] += c[k]
+            if p == "f64":
+                outs["cap"] = o
+                capped_env.append(c["capped"] > 0)
+        o50 = O.OracleEnv(model_of(i, converged_iters), cfg, dr=dr, precision="f64").step(s0, act)
+        c50 = O.ls_take("f64")
+        for k in ("searches", "capped", "stalled"):
+            counts["f64_converged_run"][k] += c50[k]
+        q5, v5 = outs["cap"]["state"][0:19], outs["cap"]["state"][19:37]
+        q50, v50 = o50["state"][0:19], o50["state"][19:37]
+        dq.append(np.abs(q5 - q50).max())
+        dv.append(np.abs(v5 - v50).max())
+        rq.append(np.abs(q5 - q50).max() / max(np.abs(q50).max(), 1e-9))
+    dq, dv, rq = map(np.array, (dq, dv, rq))
+
+    def st(x):
+        return {"p50": float(np.median(x)), "p99": float(np.percentile(x, 99)), "max": float(x.max())}
+
+    def frac(c, k):
+        return round(c[k] / max(c["searches"], 1), 5)
+
+    return {"envs": int(len(ids)), "substeps_per_env_step": int(env._n_frames), "ls_iterations": cap_iters,
+            "frac_capped": frac(counts["f64"], "capped"), "frac_stalled": frac(counts["f64"], "stalled"),
+            "frac_converged": frac(counts["f64"], "converged"),
+            "frac_capped_f32": frac(counts["f32"], "capped"),
+            "evals_per_search": round(counts["f64"]["evals"] / max(counts["f64"]["searches"], 1), 3),
+            "frac_env_steps_with_a_capped_search": round(float(np.mean(capped_env)), 4),
+            "counts": counts,
+            "vs_converged_search": {"ls_iterations": converged_iters, "qpos_abs": st(dq), "qvel_abs": st(dv),
+                                    "qpos_rel": st(rq)},
+            "note": "oracle replay of one env step from the post-window states: the fraction of Newton searches "
+                    "ended by the ls_iterations cap (alpha from PrimalSearch's undocumented exit rule) and the "
+                    "one-step state difference against the same step with the search run to convergence"}
 
 
 def contact_cap_stats(env, acts_ptr, steps):
@@ -598,7 +670,7 @@ def main():
     env.synchronize()
     barrier()
     wall = time.perf_counter() - t0
-    per_step = None
+    per_step, idle_start = None, None
     if rollout:
         # the same K steps again as K single-step launches (HIP events) from the kept start state,
         # queued right behind the timed window (the rollout's end state kept on the device first)
@@ -620,7 +692,7 @@ def main():
         # bitwise (the state record holds the rng key words as float bit patterns, some of them NaNs)
         differ = [int(f) for f, v in end.items() if not np.array_equal(env._get(f).view(np.uint32), v.view(np.uint32))]
         same = not differ
-        for b in list(end_dev.values()) + list(snap.values()):
+        for b in end_dev.values():
             b.free()
         per_step = {"launches": K, "avg_launch_ms": round(step_ms / K, 4),
                     "kernel_env_steps_per_s": round(E * K / (step_ms / 1e3), 1),
@@ -629,7 +701,30 @@ def main():
             per_step["differing_fields"] = differ
         if not (same and traj_ok):
             print(f"rank {rank}: fused rollout differs from single-step launches: {per_step}", file=sys.stderr, flush=True)
-        for b in traj:
+        # idle start (verdict r04 item 5): the same fused window from the same start state after a
+        # 0.2 s host pause, so the GPU starts it from the clock state of an idle device instead of
+        # behind the pre-warm; HIP events, like the timed window's kernel_ms.  Not `value`.  (Not in
+        # --no-extras profiling runs: their kernel stats keep to the timed launch.)
+    if rollout and not args.no_extras:
+        dev_restore(snap)
+        env.synchronize()
+        time.sleep(0.2)
+        _lib.check(L.pp3_rollout_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, K, traj[0].ptr, traj[1].ptr,
+                                       traj[2].ptr, C.byref(ms)))
+        idle_ms = ms.value
+        idle_same = np.array_equal(env._get(_abi.F_STATE).view(np.uint32), end[_abi.F_STATE].view(np.uint32))
+        idle_start = {"pause_s": 0.2, "ms_per_step": round(idle_ms / K, 4),
+                      "env_steps_per_s": round(E * K / (idle_ms / 1e3), 1),
+                      "prewarmed_ms_per_step": round(kernel_ms / K, 4),
+                      "prewarmed_env_steps_per_s": round(E * K / (kernel_ms / 1e3), 1),
+                      "idle_over_prewarmed": round(idle_ms / kernel_ms, 4), "bit_equal_to_rollout": bool(idle_same),
+                      "note": "the timed window replayed from its saved start state after a 0.2 s host pause "
+                              "(HIP events around the fused launch) vs the same launch right behind the pre-warm "
+                              "and warmup (events); value is the wall clock of the latter"}
+        if not idle_same:
+            print(f"rank {rank}: idle-start replay differs from the timed rollout", file=sys.stderr, flush=True)
+    if rollout:
+        for b in list(traj) + list(snap.values()):
             b.free()
     if policy is not None:
         # the same K steps again as the unfused loop (per step a pp3_policy_act launch on the obs
@@ -714,7 +809,9 @@ def main():
         K = args.steps
         value = E * world * K / wall_max
         launch_s = kernel_ms_max / 1e3 / K  # kernel time per env step of the batch
-        fused_policy = policy is not None and (env.config_struct.ncon_max or 8) == 8
+        # the library reports which path pp3_rollout_policy took (fused only at cap 8, action_repeat 1,
+        # PP3_POLICY_UNFUSED unset and in a product build)
+        fused_policy = policy is not None and L.pp3_rollout_policy_fused(env._h) == 1
         spl = K if (rollout or fused_policy) else 1  # env steps per launch
         bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr,
                                              trajectory=rollout or policy is not None)
@@ -769,6 +866,7 @@ def main():
                         "the same steps as per-step policy + step launches"
                         if policy is not None else "step: one pp3_step launch per env step")),
             "per_step_launch": per_step,
+            "idle_start": idle_start,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": ("pp3::env_step_kernel<8, true, 8> (policy MLP fused)" if fused_policy else
@@ -834,7 +932,8 @@ def main():
             if not (args.dr or args.obstacles or args.auto_reset or args.policy or args.gather):
                 out["host_api"] = host_api_rates(model_path, E, device, keys)
             out["contact_cap"] = contact_cap_stats(env, acts.ptr.value, min(K, 50))
-            out["one_step_err"] = one_step_err(env, dr_table=dr_table, terrain=terrain, auto_reset=args.auto_reset > 0)
+            out["one_step_err"], out["ls_cap"] = one_step_err(env, dr_table=dr_table, terrain=terrain,
+                                                              auto_reset=args.auto_reset > 0)
             out["qpos_rel_err"] = {"value": qpos_drift(env, dr_row=None if dr_table is None else dr_table[0],
                                                        terrain_row=None if terrain is None else terrain[0]),
                                    "substeps": 1000,

@@ -11,6 +11,8 @@
 
 #include <stdint.h>
 
+#include "pupper_hip.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -24,6 +26,12 @@ int pp3_phase_profile(uint64_t* host_out, int32_t n, int32_t reset);
  * HW_ID, XCC_ID, then 19 per-phase cycle counts, contacts summed over substeps, substeps that
  * used the second constraint-row slot, s_memrealtime (100 MHz) at start and end, 1 unused; then 128 phase stamps and their 128 phase ids). */
 int pp3_wave_profile(uint32_t* host_out, int32_t n);
+
+/* Which path pp3_rollout_policy takes on env `e`: 1 = ONE fused launch for the K steps
+ * (env_step_kernel<8, true, 8>), 0 = per-step policy + step launches (max_contacts = 16,
+ * action_repeat > 1, PP3_POLICY_UNFUSED=1, or a diagnostic build), -1 = null handle.  bench.py
+ * labels its policy roofline with it. */
+int32_t pp3_rollout_policy_fused(const pp3_env_t* e);
 
 #ifdef __cplusplus
 }

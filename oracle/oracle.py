@@ -119,6 +119,24 @@ def mj_forward(model, qpos, qvel, qacc_ws, ctrl, precision="f64"):
     return dict(M=M, qacc_smooth=qs, qacc=qa, qfrc_bias=qb, nefc=nefc.value, pipe=pipe)
 
 
+def ls_take(precision: str = "f64") -> dict:
+    """Line-search counters of this thread since the last call (pp3_oracle.c orc_ls_take): Newton
+    searches, their evaluations, the warm-start choice, and how each search ended -- converged
+    (ls_converged), capped (ls_iterations evaluations spent first: the alpha then comes from the
+    PrimalSearch exit rule, which MuJoCo's documentation does not specify) or stalled."""
+    out = (C.c_long * 7)()
+    lib(precision).orc_ls_take(out)
+    keys = ("evals", "searches", "smooth_starts", "starts", "converged", "capped", "stalled")
+    return dict(zip(keys, (int(v) for v in out)))
+
+
+def with_ls_iterations(model, n):
+    """Copy of the model struct with ls_iterations = n (the reference's is 5, xml:57)."""
+    m = type(model).from_buffer_copy(model)
+    m.ls_iterations = n
+    return m
+
+
 class OracleEnv:
     """Single-env oracle of PupperV3Env.reset/step operating on the device state layout."""
 

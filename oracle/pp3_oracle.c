@@ -1011,6 +1011,12 @@ static void ls_eval(LSCtx* c, LSPoint* p) {
 #define LS_NOISE ((real)64)
 static int g_ls_noise = 1;
 static _Thread_local long g_ls_total = 0, g_ls_calls = 0, g_ls_smooth = 0, g_ls_starts = 0;  /* line-search evaluations / searches (diagnostics) */
+/* how each search ended (orc_ls_take): LS_CONVERGED = a point passed ls_converged; LS_CAPPED = the
+ * evaluation budget ls_iterations ran out first, so the returned alpha is set by the exit rule below
+ * (PrimalSearch's, restated from memory of engine_solver.c: MuJoCo's documentation does not specify
+ * it); LS_STALLED = the bracket stopped shrinking (no candidate closer to the root on either side) */
+enum { LS_CONVERGED = 0, LS_CAPPED = 1, LS_STALLED = 2 };
+static _Thread_local long g_ls_exit[3] = {0, 0, 0};
 static int ls_converged(const LSPoint* p, real gtol) {
   if (RFABS(p->d0) < gtol) return 1;
   return g_ls_noise && RFABS(p->d0) <= LS_NOISE * REPS * p->d1 * RFABS(p->alpha);
@@ -1025,16 +1031,16 @@ static real line_search(LSCtx* c, real gtol, int maxit) {
   p1.alpha = p0.alpha - p0.d0 / p0.d1;
   ls_eval(c, &p1);
   if (p0.cost < p1.cost) p1 = p0;
-  if (ls_converged(&p1, gtol)) return p1.alpha;
+  if (ls_converged(&p1, gtol)) { g_ls_exit[LS_CONVERGED]++; return p1.alpha; }
   real dir = p1.d0 < 0 ? 1 : -1;
   p2 = p1;
   while (p1.d0 * dir <= -gtol && c->evals < maxit) {
     p2 = p1;
     p1.alpha -= p1.d0 / p1.d1;
     ls_eval(c, &p1);
-    if (ls_converged(&p1, gtol)) return p1.alpha;
+    if (ls_converged(&p1, gtol)) { g_ls_exit[LS_CONVERGED]++; return p1.alpha; }
   }
-  if (c->evals >= maxit) return p1.alpha;
+  if (c->evals >= maxit) { g_ls_exit[LS_CAPPED]++; return p1.alpha; }
   /* bracket [p2, p1]: p2.d0*dir < 0 < p1.d0*dir */
   p2n = p1;
   p1n.alpha = p1.alpha - p1.d0 / p1.d1;
@@ -1046,7 +1052,7 @@ static real line_search(LSCtx* c, real gtol, int maxit) {
     int best = -1;
     for (int i = 0; i < 3; i++)
       if (ls_converged(&cand[i], gtol) && (best < 0 || cand[i].cost < cand[best].cost)) best = i;
-    if (best >= 0) return cand[best].alpha;
+    if (best >= 0) { g_ls_exit[LS_CONVERGED]++; return cand[best].alpha; }
     int up1 = 0, up2 = 0;
     for (int i = 0; i < 3; i++) {
       /* tighten each bracket end with any candidate on its side that is closer to the root */
@@ -1057,6 +1063,7 @@ static real line_search(LSCtx* c, real gtol, int maxit) {
     if (up1) { p1n.alpha = p1.alpha - p1.d0 / p1.d1; ls_eval(c, &p1n); }
     if (up2) { p2n.alpha = p2.alpha - p2.d0 / p2.d1; ls_eval(c, &p2n); }
   }
+  g_ls_exit[c->evals >= maxit ? LS_CAPPED : LS_STALLED]++;
   return p1.cost < p2.cost ? p1.alpha : p2.alpha;
 }
 
@@ -1763,7 +1770,9 @@ void orc_set_ls_trace(int on) { g_ls_trace = on; }
 /* line-search evaluations and searches of this thread since the last call */
 void orc_ls_take(long* out) {
   out[0] = g_ls_total; out[1] = g_ls_calls; out[2] = g_ls_smooth; out[3] = g_ls_starts;
+  out[4] = g_ls_exit[LS_CONVERGED]; out[5] = g_ls_exit[LS_CAPPED]; out[6] = g_ls_exit[LS_STALLED];
   g_ls_total = 0; g_ls_calls = 0; g_ls_smooth = 0; g_ls_starts = 0;
+  g_ls_exit[0] = g_ls_exit[1] = g_ls_exit[2] = 0;
 }
 void orc_debug_read(double* out) { memcpy(out, g_dbg, sizeof(g_dbg)); }
 int orc_boundary_take(void) { const int n = g_boundary; g_boundary = 0; return n; }

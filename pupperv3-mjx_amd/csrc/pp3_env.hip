@@ -1140,8 +1140,9 @@ __device__ __forceinline__ float ldl_arrow_solve_b(float (&a)[NV], float rhs, in
 }
 
 // a[npos(j)] += w . J[.][j] over natural columns [J0, J1) (arrowhead Hessian rows)
-template <int J0, int J1>
-__device__ __forceinline__ void hess_acc_p(float (&a)[NV], const float (&J)[3][NV], float w0, float w1, float w2) {
+template <int J0, int J1, int W>
+__device__ __forceinline__ void hess_acc_p(float (&a)[NV], const float (&J)[3][W], float w0, float w1, float w2) {
+  static_assert(J1 <= W, "hess_acc_p: columns beyond the operand rows");
 #pragma unroll
   for (int j = J0; j < J1; j++) {  // three FMAs into the entry (not mul + 2 fma + add)
     float v = a[npos(j)];
@@ -1776,12 +1777,25 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
           // 0..3 = a leg, 4 = base only): one bit test per leg instead of two compares and an or
           const uint32_t legs = (1u << (sa & 7)) | (1u << (sb & 7));
           if (cv) {
-            const float* G = s.con_G[c];
-            const float jn = s.Jc[c][0][dn], j1 = s.Jc[c][1][dn], j2 = s.Jc[c][2][dn];
+            // the contact's G, this lane's three J entries and the 18 base-column entries in ONE
+            // pinned LDS round: unpinned, the base columns streamed three loads deep behind the
+            // weights (the last serial LDS chain on the substep's path, tools/lds_chains.py)
+            float G[5], jb[3][6];
+#pragma unroll
+            for (int k = 0; k < 5; k++) G[k] = s.con_G[c][k];
+            float jn = s.Jc[c][0][dn], j1 = s.Jc[c][1][dn], j2 = s.Jc[c][2][dn];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+              for (int j = 0; j < 6; j++) jb[r][j] = s.Jc[c][r][j];
+            PIN("+v"(G[0]), "+v"(G[1]), "+v"(G[2]), "+v"(G[3]), "+v"(G[4]), "+v"(jn), "+v"(j1), "+v"(j2),
+                "+v"(jb[0][0]), "+v"(jb[0][1]), "+v"(jb[0][2]), "+v"(jb[0][3]), "+v"(jb[0][4]), "+v"(jb[0][5]),
+                "+v"(jb[1][0]), "+v"(jb[1][1]), "+v"(jb[1][2]), "+v"(jb[1][3]), "+v"(jb[1][4]), "+v"(jb[1][5]),
+                "+v"(jb[2][0]), "+v"(jb[2][1]), "+v"(jb[2][2]), "+v"(jb[2][3]), "+v"(jb[2][4]), "+v"(jb[2][5]));
             const float w0 = jn * G[0] + j1 * G[1] + j2 * G[2];
             const float w1 = jn * G[1] + j1 * G[3];
             const float w2 = jn * G[2] + j2 * G[4];
-            hess_acc_p<0, 6>(a, s.Jc[c], w0, w1, w2);
+            hess_acc_p<0, 6>(a, jb, w0, w1, w2);
             if (legs & 1u) hess_acc_p<6, 9>(a, s.Jc[c], w0, w1, w2);
             if (legs & 2u) hess_acc_p<9, 12>(a, s.Jc[c], w0, w1, w2);
             if (legs & 4u) hess_acc_p<12, 15>(a, s.Jc[c], w0, w1, w2);
@@ -3670,6 +3684,22 @@ int pp3_rollout(pp3_env_t* e, const float* actions_dev, int64_t action_stride, i
   return launch_steps(e, actions_dev, action_stride, nsteps, reward_dev, done_dev, obs_dev, true, stream);
 }
 
+// Which path pp3_rollout_policy takes on this env: ONE fused launch (env_step_kernel<8, true, 8>)
+// unless the contact cap is 16 (its blocks do not fit 16 envs per workgroup), action_repeat > 1
+// (a wrapper step is `repeat` launches), PP3_POLICY_UNFUSED=1 (A/B) or a diagnostic build (no fused
+// policy kernel): then per-step policy + step launches.
+static bool policy_rollout_fused(const pp3_env_t* e) {
+#ifdef PP3_PHASE_PROF
+  (void)e;
+  return false;
+#else
+  const int repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;
+  return e->nc == 8 && repeat == 1 && !g_policy_unfused;
+#endif
+}
+
+int32_t pp3_rollout_policy_fused(const pp3_env_t* e) { return e ? (policy_rollout_fused(e) ? 1 : 0) : -1; }
+
 int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float* actions_dev, float* reward_dev,
                        float* done_dev, float* obs_dev, void* stream) {
   if (!e || !policy || !actions_dev) return set_err(PP3_ERR_ARG, "pp3_rollout_policy: null argument");
@@ -3680,10 +3710,8 @@ int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float
     return set_err(PP3_ERR_ARG, "pp3_rollout_policy: the policy's input width must equal the observation size 36 * observation_history");
   const size_t on = (size_t)e->N * PP3_OBS_DIM * e->H;
   const hipStream_t st = stream_of(e, stream);
-  const int repeat = e->episode_length > 0 && e->action_repeat > 1 ? e->action_repeat : 1;
-  (void)repeat;  // (the diagnostic build has no fused policy kernel)
 #ifndef PP3_PHASE_PROF
-  if (e->nc == 8 && repeat == 1 && !g_policy_unfused) {
+  if (policy_rollout_fused(e)) {
     // ONE launch for the K steps: 8-wave workgroups of 16 envs run the MLP (mlp_tile, the code of
     // pp3_policy_act) on their envs' observations before each step, then each wave steps its two
     // envs (env_step_kernel<8, true, 8>)
