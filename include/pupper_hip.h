@@ -421,6 +421,14 @@ int pp3_outputs_to_host(pp3_env_t* env, float* host);
 int pp3_host_device_ptr(void* host, void** dev_ptr);
 /* The handle's own HIP stream (hipStream_t), for ordering other work (e.g. pp3_policy_act) with it. */
 void* pp3_stream(pp3_env_t* env);
+/* Completion markers for the host API's asynchronous step (environment.py:348 `step`: the State
+ * returns at once and its obs / reward / done wait for their own step only): a HIP event (timing
+ * disabled) on the handle's device, recorded on the handle's stream; synchronize waits until every
+ * operation queued before its last record has completed (at once if never recorded). */
+int pp3_event_create(pp3_env_t* env, void** ev_out);
+int pp3_event_record(pp3_env_t* env, void* ev);
+int pp3_event_synchronize(void* ev);
+int pp3_event_destroy(void* ev);
 
 /* Small device-memory helpers so a host can run without any other GPU runtime. */
 int pp3_device_malloc(int32_t device, size_t bytes, void** out);

@@ -2372,6 +2372,18 @@ void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::Lds
 #define PP3_STEP_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
 #endif
 
+// Fused rollout, steps after the first (A/B flags): PP3_FUSED_CARRY keeps what the previous step left
+// in the env's LDS block instead of reading it back from global memory -- the state record head
+// (s.st is what was stored), the per-env parameters (load_params) and, with observation_history 2,
+// the history frame (the previous step's newest observation, s.x.e.o); PP3_ACT_PREFETCH issues
+// the next step's action load in the epilogue, after its last global-load wait.
+#ifndef PP3_FUSED_CARRY
+#define PP3_FUSED_CARRY 0
+#endif
+#ifndef PP3_ACT_PREFETCH
+#define PP3_ACT_PREFETCH 0
+#endif
+
 template <int NC, bool FUSED, int NWV = 1>
 __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     typename std::conditional<(NWV > 1), PolicyStepArgs, StepArgs>::type a_arg) {
@@ -2398,6 +2410,7 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   // the loop and kept live across it (SGPR and VGPR spills).  With FUSED false the loop runs once
   // and the kernel compiles to the single-step code it always was.
   int heavy_prev = 0;  // fused: the load flag carries over into the next step's first substep
+  float act_next = 0.0f;  // PP3_ACT_PREFETCH: this lane's action of the next fused step
   for (int it = 0;;) {
 #ifdef PP3_PHASE_PROF
   if (it == 1) pf->n = 0;  // fused launch: the stamp trace holds the second step (a warm one)
@@ -2470,6 +2483,8 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   const size_t obs_base = (size_t)env * (PP3_OBS_DIM * m.H);
   const float* oi = a.obs_in + obs_base;
   float* oo = a.obs_out + obs_base;
+  // fused steps after the first: the env's LDS block still holds what this wave left in it
+  const bool carry = PP3_FUSED_CARRY && FUSED && NWV == 1 && it > 0;
   float arow[PP3_MAX_LAG], irow[PP3_MAX_LAG], act_in = 0.0f;
   {
     const float* ar = gst + PP3_S_ACT_BUF + (l < NU ? l : 0) * m.La;
@@ -2479,7 +2494,10 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
       arow[q] = (l < NU && q < m.La) ? ar[q] : 0.0f;
       irow[q] = (l < 6 && q < m.Li) ? ir[q] : 0.0f;
     }
-    if (l < NU) act_in = act_env[l];
+    if (l < NU) {
+      if (PP3_ACT_PREFETCH && FUSED && NWV == 1 && it > 0) act_in = act_next;  // (loaded in the last epilogue)
+      else act_in = act_env[l];
+    }
   }
   LaneRec<2> re;  // plain loads (no pin): retired with the batch's first wait
   for (int k = 0; k < 2; k++)
@@ -2487,12 +2505,19 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   const KinConst kc = kin_const(m, l);  // (kept in registers for all substeps)
   // observation history: obs_out[36:] = obs_in[:36(H-1)] (environment.py:540-543)
   const int nmove = PP3_OBS_DIM * (m.H - 1);
+  // carry with H = 2: the history frame is the previous step's newest observation, still in LDS
+  const bool hist_lds = carry && nmove == PP3_OBS_DIM;
   float tmp[OBS_MOVE];
 #pragma unroll
-  for (int t = 0; t < OBS_MOVE; t++) tmp[t] = (l + HW * t < nmove) ? oi[l + HW * t] : 0.0f;
+  for (int t = 0; t < OBS_MOVE; t++) {
+    const int k = l + HW * t;
+    if (hist_lds) tmp[t] = (k < PP3_OBS_DIM) ? s.x.e.o[k < PP3_OBS_DIM ? k : 0] : 0.0f;
+    else tmp[t] = (k < nmove) ? oi[k] : 0.0f;
+  }
   float v[(PP3_S_ACT_BUF + HW - 1) / HW];  // state record head
+  if (!carry)
 #pragma unroll
-  for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++) v[t] = l + HW * t < PP3_S_ACT_BUF ? gst[l + HW * t] : 0.0f;
+    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++) v[t] = l + HW * t < PP3_S_ACT_BUF ? gst[l + HW * t] : 0.0f;
   // auto-reset mode: the previous step's done and this env's episode record (kept in LDS)
   if (a.episode) {
     if (l == 0) {
@@ -2501,10 +2526,10 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     }
     if (l < PP3_EP_STRIDE) s.ep[l] = a.episode[(size_t)env * PP3_EP_STRIDE + l];
   }
-  load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
+  if (!carry) load_params(s, m, a.dr ? a.dr + (size_t)env * PP3_NDR : nullptr, l);
   // obs is updated in place (obs_in == obs_out): every history load of this half has returned
   // before the first history store (for H >= 3 the shifted window overlaps the one it is read from)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!hist_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (own)
 #pragma unroll
     for (int t = 0; t < OBS_MOVE; t++)
@@ -2514,9 +2539,10 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
           if (PP3_MLP_OBS_LDS && PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][PP3_OBS_DIM + l + HW * t] = tmp[t];
         if (TG && to) to[PP3_OBS_DIM + l + HW * t] = tmp[t];
       }
+  if (!carry)
 #pragma unroll
-  for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
-    if (l + HW * t < PP3_S_ACT_BUF) s.st[l + HW * t] = v[t];
+    for (int t = 0; t < (PP3_S_ACT_BUF + HW - 1) / HW; t++)
+      if (l + HW * t < PP3_S_ACT_BUF) s.st[l + HW * t] = v[t];
   SYNC();
   if (l < NQ) s.qpos[l] = s.st[PP3_S_QPOS + l];
   if (l < NV) { s.qvel[l] = s.st[PP3_S_QVEL + l]; s.qws[l] = s.st[PP3_S_QACC_WS + l]; }
@@ -2704,6 +2730,12 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     r_knee = kb[1];
     r_body = kb[2];
   }
+  if (PP3_ACT_PREFETCH && FUSED && NWV == 1) {  // the next fused step's action: in flight from here on
+    // issued after the knee / body load has been waited for (the memory clobber keeps the load
+    // behind it): a wait for an older load would otherwise also wait for this one
+    asm volatile("" ::"v"(r_knee), "v"(r_body) : "memory");
+    if (it + 1 < nsteps && l < NU) act_next = (a.actions + (size_t)(it + 1) * a.act_stride + (size_t)env * NU)[l];
+  }
   r_torq = hsum(r_torq, h);
   r_jacc = hsum(r_jacc, h);
   r_mech = hsum(r_mech, h);
@@ -2820,6 +2852,8 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
     for (int i = l; i < PP3_FIRST_STRIDE; i += HW) s.st[PP3_S_QPOS + i] = fs[i];
     const float* fo = a.first_obs + (size_t)env * PP3_OBS_DIM * m.H;
     __threadfence_block();  // the prologue's history stores (other lanes, same addresses) land first
+    if (PP3_FUSED_CARRY && FUSED && NWV == 1)  // the next step's carried history frame (H = 2)
+      for (int i = l; i < PP3_OBS_DIM; i += HW) s.x.e.o[i] = fo[i];
     if (own)
       for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) {
         oo[i] = fo[i];
@@ -3764,6 +3798,30 @@ int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float
 }
 
 void* pp3_stream(pp3_env_t* e) { return e ? (void*)e->stream : nullptr; }
+
+// completion markers of the host API's asynchronous step (timing disabled: a record is one packet)
+int pp3_event_create(pp3_env_t* e, void** out) {
+  if (!e || !out) return set_err(PP3_ERR_ARG, "pp3_event_create: null argument");
+  HIPCHK(hipSetDevice(e->device));
+  hipEvent_t ev;
+  HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  *out = (void*)ev;
+  return PP3_OK;
+}
+int pp3_event_record(pp3_env_t* e, void* ev) {
+  if (!e || !ev) return set_err(PP3_ERR_ARG, "pp3_event_record: null argument");
+  HIPCHK(hipEventRecord((hipEvent_t)ev, e->stream));
+  return PP3_OK;
+}
+int pp3_event_synchronize(void* ev) {
+  if (!ev) return set_err(PP3_ERR_ARG, "pp3_event_synchronize: null event");
+  HIPCHK(hipEventSynchronize((hipEvent_t)ev));
+  return PP3_OK;
+}
+int pp3_event_destroy(void* ev) {
+  if (ev) HIPCHK(hipEventDestroy((hipEvent_t)ev));
+  return PP3_OK;
+}
 
 int pp3_set_auto_reset(pp3_env_t* e, int32_t episode_length) {
   if (!e) return set_err(PP3_ERR_ARG, "null env");

@@ -82,6 +82,13 @@ def load() -> C.CDLL:
     L.pp3_policy_last_error.restype = C.c_char_p
     L.pp3_stream.argtypes = [vp]
     L.pp3_stream.restype = vp
+    if hasattr(L, "pp3_event_create"):  # (absent from pre-round-5 builds run in kernel A/B: no host-API step there)
+        L.pp3_event_create.argtypes = [vp, C.POINTER(vp)]
+        L.pp3_event_record.argtypes = [vp, vp]
+        L.pp3_event_synchronize.argtypes = [vp]
+        L.pp3_event_destroy.argtypes = [vp]
+        for name in ("pp3_event_create", "pp3_event_record", "pp3_event_synchronize", "pp3_event_destroy"):
+            getattr(L, name).restype = C.c_int
     L.pp3_set_terrain.argtypes = [vp, vp, i32]
     L.pp3_terrain_slots.argtypes = [vp]
     L.pp3_terrain_slots.restype = i32
@@ -138,7 +145,8 @@ EXPORTED_SYMBOLS = (
     "pp3_fill_uniform", "pp3_step_timed", "pp3_rollout_timed", "pp3_set_auto_reset", "pp3_set_action_repeat",
     "pp3_policy_create", "pp3_policy_act", "pp3_policy_out_dim", "pp3_policy_destroy", "pp3_policy_last_error",
     "pp3_rollout_policy", "pp3_rollout_policy_timed",
-    "pp3_stream", "pp3_set_terrain", "pp3_terrain_slots",
+    "pp3_stream", "pp3_event_create", "pp3_event_record", "pp3_event_synchronize", "pp3_event_destroy",
+    "pp3_set_terrain", "pp3_terrain_slots",
     "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_comm_rank", "pp3_comm_world",
     "pp3_comm_last_error", "pp3_gather", "pp3_comm_allreduce", "pp3_comm_barrier",
     "pp3_render", "pp3_render_last_error",
@@ -149,18 +157,47 @@ EXPORTED_SYMBOLS = (
 DIAG_SYMBOLS = ("pp3_phase_profile", "pp3_wave_profile", "pp3_rollout_policy_fused")
 
 
+class BlockPool(list):
+    """Free PinnedBlocks of one size.  A retired pool (an unroll length the env no longer uses, a
+    closed env) frees its free blocks, and a leased block released into it later is freed at once
+    instead of being kept: nothing waits for the cyclic garbage collector."""
+
+    def __init__(self):
+        super().__init__()
+        self.retired = False
+
+    def release(self, block: "PinnedBlock") -> None:
+        if self.retired:
+            block.free()
+        else:
+            self.append(block)
+
+    def retire(self) -> None:
+        self.retired = True
+        while self:
+            self.pop().free()
+
+
+def _release(pool, block) -> None:
+    """weakref finalizer of a lease: the block goes back to its pool (or is freed there)."""
+    if isinstance(pool, BlockPool):
+        pool.release(block)
+    else:
+        pool.append(block)
+
+
 class PinnedBlock:
     """Page-locked host memory (pp3_host_malloc) exposed to numpy through __array_interface__:
-    arrays made from it keep it alive, and when the last one dies the block goes back to `pool`
-    (or is freed), so host-API output arrays never alias a block that a later step reuses."""
+    arrays made from it keep it alive, and when the last one dies the block goes back to its pool
+    (BlockPool.release), so host-API output arrays never alias a block that a later step reuses.
+    The block does not reference its pool (no reference cycle)."""
 
-    def __init__(self, nbytes: int, pool=None):
+    def __init__(self, nbytes: int):
         self.ptr = C.c_void_p()
         self.nbytes = int(nbytes)
         check(load().pp3_host_malloc(max(self.nbytes, 4), C.byref(self.ptr)))
         self.__array_interface__ = {"shape": (self.nbytes // 4,), "typestr": "<f4", "version": 3,
                                     "data": (self.ptr.value, False)}
-        self._pool = pool
         self._dev = None
 
     def device_ptr(self) -> int:
@@ -172,18 +209,22 @@ class PinnedBlock:
         return self._dev
 
     @staticmethod
-    def take(nbytes: int, pool: list) -> "PinnedBlock":
-        """A block from `pool` (a list of free blocks) or a new one; it returns there when released."""
+    def take(nbytes: int, pool: list) -> "_BlockRef":
+        """A block from `pool` (a BlockPool of free blocks) or a new one; it returns there when released."""
         import weakref
-        b = pool.pop() if pool else PinnedBlock(nbytes, pool)
+        b = pool.pop() if pool else PinnedBlock(nbytes)
         holder = _BlockRef(b)
-        weakref.finalize(holder, pool.append, b)
+        weakref.finalize(holder, _release, pool, b)
         return holder
+
+    def free(self) -> None:
+        if self.ptr:
+            load().pp3_host_free(self.ptr)
+            self.ptr = C.c_void_p()
 
     def __del__(self):
         try:
-            if self.ptr:
-                load().pp3_host_free(self.ptr)
+            self.free()
         except Exception:
             pass
 

@@ -85,6 +85,7 @@ class State:
 
 
 _LAZY = ("pipeline_state", "metrics", "info", "_record", "_metrics_raw")
+_OUTS = ("obs", "reward", "done")
 
 
 # how the host API's per-step outputs reach the host (host API): the step launch
@@ -94,6 +95,13 @@ STEP_WRITES_HOST = True
 OUTPUTS_BY_KERNEL = True
 # rollout(): trajectories up to this size are stored by the launch into page-locked host memory
 TRAJ_PINNED_MAX_BYTES = 256 << 20
+# step() returns before its launch completes (obs / reward / done wait for it on first access), with
+# at most ASYNC_DEPTH steps in flight; False: every step synchronises before it returns
+ASYNC_STEP = True
+ASYNC_DEPTH = 2
+# step(): the launch reads the actions straight from the page-locked staging block through its device
+# mapping instead of after a copy-engine transfer into a device buffer
+ACTIONS_ZERO_COPY = False
 
 
 def _ro(a):
@@ -105,18 +113,34 @@ def _ro(a):
 
 class DeviceState(State):
     """A State returned by PupperV3Env.reset / step (the host surface of the
-    device-resident env).  obs / reward / done are host arrays from the start; pipeline_state,
-    metrics, info (and the raw record) are downloaded on first access -- from the env's live
-    buffers while the env has not launched since, else from a device snapshot the env took just
-    before its next launch (PupperV3Env._before_launch), so an old state always reads its own data.
-    Every array is read-only; ``unedited()`` tells the env whether the device still holds exactly
-    this state (then step() skips the upload)."""
+    device-resident env).  step() returns before its launch has finished: obs / reward / done are
+    views of the page-locked block the launch stores into, made (after waiting for that launch's
+    completion event) on first access.  pipeline_state, metrics, info (and the raw record) are
+    downloaded on first access -- from the env's live buffers while the env has not launched since,
+    else from a device snapshot the env took just before its next launch
+    (PupperV3Env._before_launch), so an old state always reads its own data.  Every array is
+    read-only; ``unedited()`` tells the env whether the device still holds exactly this state (then
+    step() skips the upload).
 
-    def __init__(self, env: "PupperV3Env", gen: int, single: bool, obs, reward, done):
-        self.__dict__.update(obs=obs, reward=reward, done=done, _env=env, _gen=gen, _single=single, _snap=None,
-                             _ids=None, _out=(obs, reward, done))
+    Assigning a field is an edit (the next step uploads the state).  Assigning one of the lazy
+    fields (pipeline_state, info, metrics) of a state not yet read first downloads the whole lazy
+    part (a blocking copy of the state record, metrics and pipeline record, plus a stream sync for
+    a snapshot), so the assigned value is what a later read sees; obs / reward / done likewise wait
+    for their step first.  A wrapper that assigns state.info every step therefore pays one lazy
+    download per step."""
+
+    def __init__(self, env: "PupperV3Env", gen: int, single: bool, obs=None, reward=None, done=None, ready=None):
+        d = dict(_env=env, _gen=gen, _single=single, _snap=None, _ids=None, _ready=ready)
+        if ready is None:  # outputs already on the host
+            d.update(obs=obs, reward=reward, done=done, _out=(obs, reward, done))
+        else:  # (lease, completion event slot): views made on first access
+            d.update(_out=None)
+        self.__dict__.update(d)
 
     def __getattr__(self, name):
+        if name in _OUTS and self.__dict__.get("_ready") is not None:
+            self._wait_outputs()
+            return self.__dict__[name]
         if name in _LAZY and "_env" in self.__dict__:
             self._materialize()
             return self.__dict__[name]
@@ -129,14 +153,28 @@ class DeviceState(State):
     def __setattr__(self, name, value):
         # assigning a lazy field (pipeline_state, info, metrics, ...) of a state not yet read: fetch
         # the issued values first, so the assignment is an edit unedited() sees and nothing
-        # downloaded later overwrites it
+        # downloaded later overwrites it (see the class docstring for the cost)
+        if name in _OUTS and self.__dict__.get("_ready") is not None:
+            self._wait_outputs()
         if name in _LAZY and "_env" in self.__dict__ and not self.materialized:
             self._materialize()
         object.__setattr__(self, name, value)
 
+    def _wait_outputs(self) -> None:
+        """obs / reward / done of a state whose launch may still run: wait for its completion event,
+        then view the page-locked block the launch stored them into."""
+        ready = self.__dict__.get("_ready")
+        if ready is None:
+            return
+        lease, slot = ready
+        slot.wait()
+        obs, rew, done = self._env._output_views(lease, self._single)
+        self.__dict__.update(obs=obs, reward=rew, done=done, _out=(obs, rew, done), _ready=None)
+
     def _materialize(self) -> None:
         if self.materialized:
             return
+        self._wait_outputs()  # (the launch has completed: its fields are final)
         env = self._env
         src = self._snap
         if src is None and env._gen != self._gen:
@@ -157,6 +195,8 @@ class DeviceState(State):
 
     def unedited(self) -> bool:
         """True when every array step() would upload is the very object this state was issued with."""
+        if self.__dict__.get("_ready") is not None:  # outputs not yet viewed: nothing can have been assigned
+            return True
         if any(self.__dict__.get(k) is not o for k, o in zip(("obs", "reward", "done"), self._out)):
             return False
         if not self.materialized:
@@ -366,10 +406,12 @@ class PupperV3Env:
         self._gen = 0
         self._issued = None
         self._snap_pool = []
-        self._pin_pool = []    # page-locked output blocks (obs | reward | done) of issued states
+        self._pin_pool = _lib.BlockPool()  # page-locked output blocks (obs | reward | done) of issued states
         self._traj_pool = {}   # page-locked rollout trajectory blocks, per unroll length
-        self._act_stage = _lib.PinnedBlock(self.num_envs * _abi.NU * 4)  # page-locked action staging
-        self._act_stage_arr = np.asarray(self._act_stage)
+        # page-locked action staging: a ring of ASYNC_DEPTH blocks, each reused only after the launch
+        # that read it has completed (its event)
+        self._act_ring = [_ActSlot(self, self.num_envs * _abi.NU * 4) for _ in range(max(1, ASYNC_DEPTH))]
+        self._act_i = 0
         self._lazy_extra = {}  # field id -> info hook (wrappers.AutoResetEpisodeEnv: the episode record)
         self._issue_capture = None  # () -> host data a wrapper attaches to each state when it is issued
         self._field_elems = {f: self.device_field(f)[1] for f in (_abi.F_STATE, _abi.F_METRICS, _abi.F_PIPELINE)}
@@ -471,9 +513,13 @@ class PupperV3Env:
             b.free()
         self._roll_bufs = None
         # free page-locked blocks go with their pools; leased ones are freed when their arrays die
-        for pool in (getattr(self, "_pin_pool", None), getattr(self, "_traj_pool", None)):
-            if pool is not None:
-                pool.clear()
+        if getattr(self, "_pin_pool", None) is not None:
+            self._pin_pool.retire()
+        for pool in (getattr(self, "_traj_pool", None) or {}).values():
+            pool.retire()
+        for slot in getattr(self, "_act_ring", None) or ():
+            slot.close()
+        self._act_ring = None
 
     def __del__(self):
         try:
@@ -556,16 +602,25 @@ class PupperV3Env:
         return self._issue(single)
 
     def step(self, state: State, action) -> State:
-        single = np.ndim(state.reward) == 0
+        single = _single_of(state)
         act = np.ascontiguousarray(np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU))
         if not self.holds(state):
             self._write_state(state)
-        # actions through a page-locked staging block, copied on the env's stream ahead of the launch
-        np.copyto(self._act_stage_arr, act.reshape(-1))
-        _lib.check(self._L.pp3_memcpy_h2d_async(self._act_buf.ptr, self._act_stage.ptr, act.nbytes,
-                                                 self._L.pp3_stream(self._h)))
+        # actions through a page-locked staging block of the ring; the launch that last read this
+        # block has completed once its event has (at most ASYNC_DEPTH steps in flight)
+        slot = self._act_ring[self._act_i]
+        self._act_i = (self._act_i + 1) % len(self._act_ring)
+        slot.wait()
+        np.copyto(slot.arr, act.reshape(-1))
+        if ACTIONS_ZERO_COPY:
+            act_ptr = C.c_void_p(slot.block.device_ptr())
+        else:  # copied on the env's stream ahead of the launch
+            _lib.check(self._L.pp3_memcpy_h2d_async(self._act_buf.ptr, slot.block.ptr, act.nbytes,
+                                                     self._L.pp3_stream(self._h)))
+            act_ptr = self._act_buf.ptr
         if not STEP_WRITES_HOST:
-            self.step_device(self._act_buf.ptr.value)
+            self.step_device(act_ptr.value)
+            slot.record()
             return self._issue(single)
         # the step launch itself stores obs | reward | done into the page-locked output block (a
         # one-step pp3_rollout whose trajectory rows are the block's device mapping): no copy after it
@@ -573,8 +628,11 @@ class PupperV3Env:
         lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
         dev = lease.device_ptr()
         self._before_launch()
-        _lib.check(self._L.pp3_rollout(self._h, self._act_buf.ptr, 0, 1, C.c_void_p(dev + 4 * n * D),
+        _lib.check(self._L.pp3_rollout(self._h, act_ptr, 0, 1, C.c_void_p(dev + 4 * n * D),
                                        C.c_void_p(dev + 4 * n * (D + 1)), C.c_void_p(dev), None))
+        slot.record()
+        if ASYNC_STEP:  # no host sync: the State's outputs wait for this event when first read
+            return self._issue(single, lease, slot)
         return self._issue(single, lease)
 
     def rollout_device(self, actions_dev: int, action_stride: int, nsteps: int, reward_dev: Optional[int] = None,
@@ -594,7 +652,7 @@ class PupperV3Env:
         the last step (what K step() calls return) and the per-step trajectory {"obs": [K, N, 36H],
         "reward": [K, N], "done": [K, N]} (single-env states: [K, 36H] / [K]).  Bit for bit the
         same as K step() calls."""
-        single = np.ndim(state.reward) == 0
+        single = _single_of(state)
         n, D = self.num_envs, self.observation_size
         act = np.ascontiguousarray(np.asarray(actions, dtype=np.float32))
         if act.ndim < 2 or act.size % (n * _abi.NU):
@@ -632,7 +690,7 @@ class PupperV3Env:
         before each of the `nsteps` steps; no host round trip until the end.  Returns the state
         after the last step and {"obs": [K, N, 36H], "action": [K, N, 12], "reward": [K, N],
         "done": [K, N]} (single-env states: without the N axis)."""
-        single = np.ndim(state.reward) == 0
+        single = _single_of(state)
         n, D, K = self.num_envs, self.observation_size, int(nsteps)
         if K < 1:
             raise ValueError("nsteps must be >= 1")
@@ -666,8 +724,10 @@ class PupperV3Env:
         if nbytes > TRAJ_PINNED_MAX_BYTES:
             return None
         for k in [k for k in self._traj_pool if k != K]:  # keep free blocks of the current length only
-            del self._traj_pool[k]
-        lease = _lib.PinnedBlock.take(nbytes, self._traj_pool.setdefault(K, []))
+            self._traj_pool.pop(k).retire()  # (its leased blocks are freed when released)
+        if K not in self._traj_pool:
+            self._traj_pool[K] = _lib.BlockPool()
+        lease = _lib.PinnedBlock.take(nbytes, self._traj_pool[K])
         dev = lease.device_ptr()
         return lease, (dev, dev + 4 * K * n * D, dev + 4 * K * n * (D + 1))
 
@@ -711,10 +771,28 @@ class PupperV3Env:
         _lib.check(self._L.pp3_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(src_dev), out.nbytes))
         return out
 
-    def _issue(self, single: bool, lease=None) -> DeviceState:
-        # obs | reward | done land in one page-locked block (one sync); the arrays are views of it
-        # and keep it leased until the last of them dies.  `lease`: a block the launch already fills
+    def _output_views(self, lease, single: bool):
+        """(obs, reward, done): read-only views of a filled page-locked output block; they keep it
+        leased until the last of them dies."""
         n, D = self.num_envs, self.observation_size
+        flat = np.asarray(lease)
+        obs = _ro(flat[:n * D].reshape(n, D))
+        rew = _ro(flat[n * D:n * (D + 1)])
+        done = _ro(flat[n * (D + 1):])
+        if single:
+            obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
+        return obs, rew, done
+
+    def _issue(self, single: bool, lease=None, slot=None) -> DeviceState:
+        # obs | reward | done land in one page-locked block (one sync); the arrays are views of it
+        # and keep it leased until the last of them dies.  `lease`: a block the launch already fills;
+        # with `slot` (its completion event) the state is returned at once and waits on first read
+        n, D = self.num_envs, self.observation_size
+        if slot is not None:
+            st = DeviceState(self, self._gen, single, ready=(lease, slot))
+            st.__dict__["_capture"] = self._issue_capture() if self._issue_capture is not None else None
+            self._issued = weakref.ref(st)
+            return st
         if lease is None:
             lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
             base = lease.ptr.value
@@ -725,12 +803,7 @@ class PupperV3Env:
                                    (_abi.F_DONE, 4 * n * (D + 1), 4 * n)):
                     _lib.check(self._L.pp3_copy_field_to_host_async(self._h, f, C.c_void_p(base + off), nb))
         self.synchronize()
-        flat = np.asarray(lease)
-        obs = _ro(flat[:n * D].reshape(n, D))
-        rew = _ro(flat[n * D:n * (D + 1)])
-        done = _ro(flat[n * (D + 1):])
-        if single:
-            obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
+        obs, rew, done = self._output_views(lease, single)
         st = DeviceState(self, self._gen, single, obs, rew, done)
         st.__dict__["_capture"] = self._issue_capture() if self._issue_capture is not None else None
         self._issued = weakref.ref(st)
@@ -839,6 +912,42 @@ class PupperV3Env:
         put(io, info["imu_buffer"], 6 * Li)
         self._put(_abi.F_STATE, rec)
         self._put(_abi.F_OBS, np.asarray(state.obs, dtype=np.float32).reshape(n, -1))
+
+
+def _single_of(state) -> bool:
+    """A single-env state (reset with one key): from the DeviceState's flag when it has one, so a
+    pending state's outputs are not waited for just to learn their shape."""
+    d = getattr(state, "__dict__", {})
+    if "_single" in d:
+        return bool(d["_single"])
+    return np.ndim(state.reward) == 0
+
+
+class _ActSlot:
+    """One page-locked action staging block of PupperV3Env.step's ring and the completion event of
+    the last launch that read it (pp3_event_*)."""
+
+    def __init__(self, env: "PupperV3Env", nbytes: int):
+        self._L = env._L
+        self._h = env._h
+        self.block = _lib.PinnedBlock(nbytes)
+        self.arr = np.asarray(self.block)
+        ev = C.c_void_p()
+        _lib.check(self._L.pp3_event_create(env._h, C.byref(ev)))
+        self.ev = ev
+
+    def record(self) -> None:
+        _lib.check(self._L.pp3_event_record(self._h, self.ev))
+
+    def wait(self) -> None:
+        if self.ev:
+            _lib.check(self._L.pp3_event_synchronize(self.ev))
+
+    def close(self) -> None:
+        if self.ev:
+            self._L.pp3_event_destroy(self.ev)
+            self.ev = C.c_void_p()
+        self.block.free()
 
 
 def _squeeze_tree(v):

@@ -229,3 +229,68 @@ def test_wrapper_states_keep_their_first_state(require_gpu):
         np.testing.assert_array_equal(s2.info["first_obs"], w._first_obs)
     finally:
         w.env.close()
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_async_steps_match_synchronous_steps(require_gpu, zero_copy):
+    """step() returns before its launch completes (ASYNC_STEP): states issued back to back and read
+    only afterwards hold their own step's obs / reward / done / record, bit for bit the same as a
+    loop that synchronises every step; with the actions read by the launch straight from the
+    page-locked staging ring too (ACTIONS_ZERO_COPY), and through the wrapper."""
+    from pupperv3_mjx import environment
+    saved = environment.ASYNC_STEP, environment.ACTIONS_ZERO_COPY
+    acts = np.random.RandomState(9).uniform(-1, 1, size=(7, N, 12)).astype(np.float32)
+    try:
+        for wrapped in (False, True):
+            ref = []
+            environment.ASYNC_STEP, environment.ACTIONS_ZERO_COPY = False, False
+            e = _env()
+            api = wrappers.wrap(e, episode_length=5) if wrapped else e
+            st = api.reset(make_keys(11, N))
+            for t in range(7):
+                st = api.step(st, acts[t])
+                ref.append((np.array(st.obs), np.array(st.reward), np.array(st.done), np.array(st._record)))
+            e.close()
+            environment.ASYNC_STEP, environment.ACTIONS_ZERO_COPY = True, zero_copy
+            e = _env()
+            api = wrappers.wrap(e, episode_length=5) if wrapped else e
+            st = api.reset(make_keys(11, N))
+            kept = []
+            for t in range(7):
+                st = api.step(st, acts[t])
+                kept.append(st)
+            assert all(k.__dict__.get("_ready") is not None for k in kept[-2:])  # returned unread
+            for k, (o, r, d, rec) in zip(kept, ref):
+                np.testing.assert_array_equal(k.obs, o)
+                np.testing.assert_array_equal(k.reward, r)
+                np.testing.assert_array_equal(k.done, d)
+                np.testing.assert_array_equal(k._record, rec)
+            e.close()
+    finally:
+        environment.ASYNC_STEP, environment.ACTIONS_ZERO_COPY = saved
+
+
+def test_retired_pools_free_their_blocks(require_gpu):
+    """A page-locked block leased from a pool the env has retired (a trajectory length no longer
+    used, or a closed env) is freed when released, not parked in the orphaned pool (advisor r04)."""
+    from pupperv3_mjx import _lib
+    e = _env()
+    try:
+        st = e.reset(make_keys(3, N))
+        st, tr3 = e.rollout(st, np.zeros((3, N, 12), np.float32))
+        pool3 = e._traj_pool[3]
+        st, tr4 = e.rollout(st, np.zeros((4, N, 12), np.float32))
+        assert 3 not in e._traj_pool and pool3.retired and len(pool3) == 0
+        blk = tr3["obs"].base
+        while blk is not None and not isinstance(blk, _lib._BlockRef):
+            blk = getattr(blk, "base", None)
+        block = blk.block if blk is not None else None
+        del tr3, blk
+        import gc
+        gc.collect()
+        assert len(pool3) == 0
+        if block is not None:
+            assert not block.ptr  # freed on release
+    finally:
+        e.close()
+    assert e._pin_pool.retired

@@ -239,6 +239,9 @@ def test_obs_pointer_stable_across_steps(model_path):
         st = e.step(st, a)
         st = e.step(st, a)
         assert e.device_field(_abi.F_OBS)[0] == ptr0
+        # step() returns before its launch completes: a raw read of the device buffer (not through
+        # the State) synchronises with the env's stream first
+        e.synchronize()
         host = np.empty((4, n_per), np.float32)
         _lib.check(e._L.pp3_memcpy_d2h(host.ctypes.data_as(C.c_void_p), C.c_void_p(ptr0), host.nbytes))
         np.testing.assert_array_equal(host, st.obs)

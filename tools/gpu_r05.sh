@@ -28,13 +28,23 @@ for step in "$@"; do
       REPS=${REPS:-4} STEPS=20 bash tools/ab_bench.sh > $OUT/ab_driver.txt 2>&1 || { tail $OUT/ab_driver.txt; exit 1; }
       cat $OUT/ab_driver.txt ;;
     hostapi)
-      timeout -k 10 200 python tools/host_api_trace.py 200 1 > $OUT/host_api_plain.txt 2>&1 || { tail $OUT/host_api_plain.txt; exit 1; }
+      for mode in sync async async_zc sync async async_zc; do
+        for pipe in 1 0; do
+          timeout -k 10 200 python tools/host_api_trace.py 200 $pipe $mode >> $OUT/host_api_plain.txt 2>&1 || { tail $OUT/host_api_plain.txt; exit 1; }
+        done
+      done
       cat $OUT/host_api_plain.txt
-      timeout -k 10 240 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/host_api_trace -o run --output-format csv -- python3 tools/host_api_trace.py 200 1 > $OUT/host_api_trace.log 2>&1 || { tail $OUT/host_api_trace.log; exit 1; }
-      grep "env.step" $OUT/host_api_trace.log ;;
+      for mode in sync async; do
+        timeout -k 10 240 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/host_api_trace_$mode -o run --output-format csv -- python3 tools/host_api_trace.py 200 1 $mode > $OUT/host_api_trace_$mode.log 2>&1 || { tail $OUT/host_api_trace_$mode.log; exit 1; }
+        grep "env.step" $OUT/host_api_trace_$mode.log
+      done ;;
     prof)
       bash tools/gpu_profile.sh $TAG/prof > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; }
       tail -30 $OUT/prof.log ;;
+    phases)
+      PP3_DIAG_OUT=$OUT DIAG_FUSED=1 timeout -k 10 300 python tests/diag_phases.py > $OUT/phases_fused.txt 2>&1 || { tail $OUT/phases_fused.txt; exit 1; }
+      head -22 $OUT/phases_fused.txt
+      python tools/trace_intervals.py $OUT/waves.npy 10,12,11,17,18,0 > $OUT/phases_fused_intervals.txt 2>&1; head -40 $OUT/phases_fused_intervals.txt ;;
     policy)
       timeout -k 10 300 python bench.py --policy 256,128,128 > $OUT/bench_policy.json 2> $OUT/bench_policy.err || { tail $OUT/bench_policy.err; exit 1; }
       python tools/bench_summary.py $OUT/bench_policy.json

@@ -2,7 +2,12 @@
 the host API's time per step goes).  4096 envs (bench.py workload), 20 untimed steps, then `N`
 timed env.step(state, numpy actions) calls; prints us/step.
 
-  python tools/host_api_trace.py [N] [pipeline_output 0|1]
+  python tools/host_api_trace.py [N] [pipeline_output 0|1] [sync|async|async_zc]
+
+Modes: sync = every step synchronises before it returns (the round-4 host API); async = step()
+returns at once, obs / reward / done wait for their own launch (environment.ASYNC_STEP); async_zc =
+async, and the launch reads the actions straight from the page-locked staging block
+(environment.ACTIONS_ZERO_COPY).
 """
 import os
 import sys
@@ -13,12 +18,15 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "pupperv3-mjx_amd")]
 import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
-from pupperv3_mjx import MODEL_XML, sharding  # noqa: E402
+from pupperv3_mjx import MODEL_XML, environment, sharding  # noqa: E402
 from pupperv3_mjx.environment import PupperV3Env  # noqa: E402
 
 E = 4096
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 pipe = (sys.argv[2] == "1") if len(sys.argv) > 2 else True
+mode = sys.argv[3] if len(sys.argv) > 3 else "async"
+environment.ASYNC_STEP = mode != "sync"
+environment.ACTIONS_ZERO_COPY = mode == "async_zc"
 env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=pipe)
 acts = np.random.RandomState(3).uniform(-1, 1, size=(N + 20, E, 12)).astype(np.float32)
 st = env.reset(sharding.shard_keys(0, E, 1, 0))
@@ -30,6 +38,6 @@ for i in range(N):
     st = env.step(st, acts[20 + i])
 _ = np.asarray(st.obs).sum()
 dt = time.perf_counter() - t
-print(f"env.step x {N} (pipeline_output={pipe}): {dt / N * 1e6:.1f} us/step = {E * N / dt / 1e6:.2f} M env-steps/s",
+print(f"env.step x {N} (pipeline_output={pipe}, {mode}): {dt / N * 1e6:.1f} us/step = {E * N / dt / 1e6:.2f} M env-steps/s",
       flush=True)
 env.close()

@@ -17,7 +17,7 @@ def main():
     if len(sys.argv) == 1:
         subprocess.run(["make", "-s", "-C", CSRC, "asm-prof"], check=True)
     s = open(path).read()
-    a = s.index("_ZN3pp315env_step_kernelILi8EEEvNS_8StepArgsE:")
+    a = s.index("_ZN3pp315env_step_kernelILi8ELb1ELi1EEEvNSt11conditionalIXgtT1_Li1EENS_14PolicyStepArgsENS_8StepArgsEE4typeE:")
     body = s[a:s.index(".Lfunc_end", a)].split("\n")
     seg = Counter()
     out = []
