@@ -41,6 +41,11 @@ constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + HW - 1) / HW;
 constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
 constexpr int NHIT = 64;        // contact-overflow ranking window (hits kept for ranking)
 constexpr float LS_NOISE = 64.0f;  // line-search convergence floor, in roundoffs of alpha (oracle LS_NOISE)
+// PP3_LS_E0: the line search's first evaluation (alpha = 0) summed together with the search
+// direction's quadratics (bitwise equal, +0.3 % fused; 0 = after them, as an evaluation of its own)
+#ifndef PP3_LS_E0
+#define PP3_LS_E0 1
+#endif
 
 // Phase-local scratch that never lives across a phase boundary it does not own.
 template <int NC>
@@ -1850,17 +1855,11 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
 #ifdef PP3_PHASE_PROF
     if (pf && NR > 1 && rowany[NR - 1]) pf->slot2++;
 #endif
-    q1 = hsum(q1, h);
-    q2 = hsum(q2, h);
-    sn = sqrtf(hsum(sn, h));
-    live = live && !(sn < MINVAL);
-    const float gtol = m.gtol_scale * sn;
-    // cost and derivatives of the 1-D piecewise quadratic at alpha (alpha is per half)
-    auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
+    // this half's row pieces of the 1-D piecewise quadratic at alpha (alpha is per half)
+    auto pieces = [&](float alpha, float& t0, float& t1, float& t2) {
       // row slot 0 always holds rows (the NFR frictionloss rows come first): its pieces start the
       // sums instead of being added to zeros
       static_assert(NFR > 0, "row slot 0 is never empty");
-      float t0, t1, t2;
 #pragma unroll
       for (int t = 0; t < NR; t++) {
         if (t > 0 && !rowany[t]) continue;
@@ -1872,12 +1871,34 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
         if (t == 0) { t0 = p0; t1 = p1; t2 = p2; }
         else { t0 += p0; t1 += p1; t2 += p2; }
       }
-      t0 = hsum(t0, h) + gauss;
-      t1 = hsum(t1, h) + q1;
-      t2 = hsum(t2, h) + q2;
+    };
+    // cost and derivatives at alpha from the half-summed pieces
+    auto finish = [&](float alpha, float t0, float t1, float t2, float& cost, float& d0, float& d1) {
+      t0 = t0 + gauss;
+      t1 = t1 + q1;
+      t2 = t2 + q2;
       cost = t0 + alpha * t1 + alpha * alpha * t2;
       d0 = t1 + 2.0f * alpha * t2;
       d1 = fmaxf(2.0f * t2, MINVAL);
+    };
+#if PP3_LS_E0
+    // the first evaluation (alpha = 0) needs nothing the direction's sums produce: its three sums
+    // run beside them (six independent DPP chains) instead of after them
+    float e0s0, e0s1, e0s2;
+    pieces(0.0f, e0s0, e0s1, e0s2);
+    e0s0 = hsum(e0s0, h);
+    e0s1 = hsum(e0s1, h);
+    e0s2 = hsum(e0s2, h);
+#endif
+    q1 = hsum(q1, h);
+    q2 = hsum(q2, h);
+    sn = sqrtf(hsum(sn, h));
+    live = live && !(sn < MINVAL);
+    const float gtol = m.gtol_scale * sn;
+    auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
+      float t0, t1, t2;
+      pieces(alpha, t0, t1, t2);
+      finish(alpha, hsum(t0, h), hsum(t1, h), hsum(t2, h), cost, d0, d1);
     };
     // converged at (alpha, d0, d1): MuJoCo's |d0| < gtol, or the remaining Newton correction
     // |d0 / d1| within LS_NOISE roundoffs of alpha -- the fp32 floor below which the search would
@@ -1892,7 +1913,11 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     if (live) {
       const int maxit = m.ls_iterations;
       float c0, g0, h0;
+#if PP3_LS_E0
+      finish(0.0f, e0s0, e0s1, e0s2, c0, g0, h0);
+#else
       eval(0.0f, c0, g0, h0);
+#endif
       evals++;
       float a1 = -g0 / h0, c1, g1, h1;
       eval(a1, c1, g1, h1);
@@ -2372,13 +2397,14 @@ void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::Lds
 #define PP3_STEP_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
 #endif
 
-// Fused rollout, steps after the first (A/B flags): PP3_FUSED_CARRY keeps what the previous step left
+// Fused rollout, steps after the first: PP3_FUSED_CARRY (default 1: bitwise equal, +0.6 % over 200 fused
+// steps and +0.7 % at the driver's window, profiles/AB_LOG.md round 5) keeps what the previous step left
 // in the env's LDS block instead of reading it back from global memory -- the state record head
 // (s.st is what was stored), the per-env parameters (load_params) and, with observation_history 2,
 // the history frame (the previous step's newest observation, s.x.e.o); PP3_ACT_PREFETCH issues
-// the next step's action load in the epilogue, after its last global-load wait.
+// the next step's action load in the epilogue, after its last global-load wait (measured -0.3 %: off).
 #ifndef PP3_FUSED_CARRY
-#define PP3_FUSED_CARRY 0
+#define PP3_FUSED_CARRY 1
 #endif
 #ifndef PP3_ACT_PREFETCH
 #define PP3_ACT_PREFETCH 0

@@ -101,7 +101,12 @@ ASYNC_STEP = True
 ASYNC_DEPTH = 2
 # step(): the launch reads the actions straight from the page-locked staging block through its device
 # mapping instead of after a copy-engine transfer into a device buffer
-ACTIONS_ZERO_COPY = False
+ACTIONS_ZERO_COPY = True
+# step() (with ASYNC_STEP) queues its launch and issues it at the env's next device operation (the
+# next step, any other call into the library, or the first read of the returned state's fields): by
+# then the caller of `state = env.step(state, action)` has dropped the state the launch overwrites,
+# so no device snapshot of it is taken (PupperV3Env._flush)
+DEFER_LAUNCH = True
 
 
 def _ro(a):
@@ -161,12 +166,13 @@ class DeviceState(State):
         object.__setattr__(self, name, value)
 
     def _wait_outputs(self) -> None:
-        """obs / reward / done of a state whose launch may still run: wait for its completion event,
-        then view the page-locked block the launch stored them into."""
+        """obs / reward / done of a state whose launch may still run (or still be queued): issue it,
+        wait for its completion event, then view the page-locked block the launch stored them into."""
         ready = self.__dict__.get("_ready")
         if ready is None:
             return
         lease, slot = ready
+        self._env._flush_for(self)
         slot.wait()
         obs, rew, done = self._env._output_views(lease, self._single)
         self.__dict__.update(obs=obs, reward=rew, done=done, _out=(obs, rew, done), _ready=None)
@@ -180,11 +186,11 @@ class DeviceState(State):
         if src is None and env._gen != self._gen:
             raise RuntimeError("DeviceState: the env launched again without preserving this state (internal error)")
         if src is not None:
-            env.synchronize()  # the snapshot's d2d copies were queued on the env's stream
+            _lib.check(env._raw.pp3_synchronize(env._h))  # the snapshot's d2d copies were queued on the env's stream
         fields = env._lazy_fields()
         got = {}
-        for f in fields:
-            got[f] = env._download(f, src.ptr.value + env._snap_offsets[f] if src is not None else None)
+        for f in fields:  # (raw library calls: a step queued after this state stays queued, DEFER_LAUNCH)
+            got[f] = env._download(f, src.ptr.value + env._snap_offsets[f] if src is not None else None, raw=True)
         lazy = env._unpack_lazy(self, got, self._single)
         for k, v in lazy.items():  # never over a value the caller already assigned
             self.__dict__.setdefault(k, v)
@@ -392,7 +398,9 @@ class PupperV3Env:
         h = C.c_void_p()
         _lib.check(L.pp3_create(C.byref(m), C.byref(c), self.num_envs, self.device, C.byref(h)))
         self._h = h
-        self._L = L
+        self._raw = L
+        self._pending = None
+        self._L = _FlushingLib(self, L)  # every call into the library issues a queued step first
         assert int(L.pp3_state_stride(h)) == self.stride
         _lib.check(L.pp3_set_pipeline_output(h, int(pipeline_output)))
         self._keys_buf = _lib.DeviceBuffer(self.num_envs * 8, self.device)
@@ -405,6 +413,8 @@ class PupperV3Env:
         buffers, the last issued state, and a pool of device snapshots of its lazy fields."""
         self._gen = 0
         self._issued = None
+        self._pending = None  # a step() launch queued for the next device operation (DEFER_LAUNCH)
+        self._n_snapshots = 0  # device snapshots taken of issued states (_before_launch)
         self._snap_pool = []
         self._pin_pool = _lib.BlockPool()  # page-locked output blocks (obs | reward | done) of issued states
         self._traj_pool = {}   # page-locked rollout trajectory blocks, per unroll length
@@ -575,10 +585,13 @@ class PupperV3Env:
     def synchronize(self) -> None:
         _lib.check(self._L.pp3_synchronize(self._h))
 
-    def _get(self, field_id: int, dtype=np.float32) -> np.ndarray:
-        _, n = self.device_field(field_id)
-        out = np.empty((self.num_envs, n), dtype=np.float32)
-        _lib.check(self._L.pp3_copy_field_to_host(self._h, field_id, out.ctypes.data_as(C.c_void_p), out.nbytes))
+    def _get(self, field_id: int, dtype=np.float32, raw: bool = False) -> np.ndarray:
+        """A field of the device buffers (after the queued step, if any; `raw`: as they are now)."""
+        L = self._raw if raw else self._L
+        p, n = C.c_void_p(), C.c_int64()
+        _lib.check(L.pp3_field(self._h, field_id, C.byref(p), C.byref(n)))
+        out = np.empty((self.num_envs, n.value), dtype=np.float32)
+        _lib.check(L.pp3_copy_field_to_host(self._h, field_id, out.ctypes.data_as(C.c_void_p), out.nbytes))
         return out
 
     def _put(self, field_id: int, arr: np.ndarray) -> None:
@@ -602,6 +615,7 @@ class PupperV3Env:
         return self._issue(single)
 
     def step(self, state: State, action) -> State:
+        self._flush()
         single = _single_of(state)
         act = np.ascontiguousarray(np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU))
         if not self.holds(state):
@@ -627,6 +641,12 @@ class PupperV3Env:
         n, D = self.num_envs, self.observation_size
         lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
         dev = lease.device_ptr()
+        if ASYNC_STEP and DEFER_LAUNCH:
+            # the state this launch will leave on the device (its generation is the env's after it)
+            st = DeviceState(self, self._gen + 1, single, ready=(lease, slot))
+            st.__dict__["_capture"] = self._issue_capture() if self._issue_capture is not None else None
+            self._pending = (act_ptr.value, dev, slot, weakref.ref(st))
+            return st
         self._before_launch()
         _lib.check(self._L.pp3_rollout(self._h, act_ptr, 0, 1, C.c_void_p(dev + 4 * n * D),
                                        C.c_void_p(dev + 4 * n * (D + 1)), C.c_void_p(dev), None))
@@ -646,12 +666,35 @@ class PupperV3Env:
         _lib.check(self._L.pp3_rollout(self._h, C.c_void_p(actions_dev), int(action_stride), int(nsteps),
                                        vp(reward_dev), vp(done_dev), vp(obs_dev), vp(stream)))
 
+    def _flush_for(self, st: "DeviceState") -> None:
+        """Issue the queued launch if `st` is the state it returns (its outputs are wanted)."""
+        p = self._pending
+        if p is not None and p[3]() is st:
+            self._flush()
+
+    def _flush(self) -> None:
+        """Issue the step() launch queued by DEFER_LAUNCH (no-op when none is): first the device
+        snapshot of the state it overwrites, if that state is still alive and unread
+        (_before_launch), then the launch and its completion event."""
+        p = self._pending
+        if p is None:
+            return
+        self._pending = None
+        act, dev, slot, stref = p
+        self._before_launch()
+        n, D = self.num_envs, self.observation_size
+        _lib.check(self._raw.pp3_rollout(self._h, C.c_void_p(act), 0, 1, C.c_void_p(dev + 4 * n * D),
+                                         C.c_void_p(dev + 4 * n * (D + 1)), C.c_void_p(dev), None))
+        slot.record()
+        self._issued = stref
+
     def rollout(self, state: State, actions) -> Tuple[State, Dict[str, np.ndarray]]:
         """The unroll of brax's generate_unroll ([ext] brax 0.12.1 training/acting.py: a lax.scan of
         env.step) with the K actions given up front, as ONE fused launch: returns the state after
         the last step (what K step() calls return) and the per-step trajectory {"obs": [K, N, 36H],
         "reward": [K, N], "done": [K, N]} (single-env states: [K, 36H] / [K]).  Bit for bit the
         same as K step() calls."""
+        self._flush()
         single = _single_of(state)
         n, D = self.num_envs, self.observation_size
         act = np.ascontiguousarray(np.asarray(actions, dtype=np.float32))
@@ -690,6 +733,7 @@ class PupperV3Env:
         before each of the `nsteps` steps; no host round trip until the end.  Returns the state
         after the last step and {"obs": [K, N, 36H], "action": [K, N, 12], "reward": [K, N],
         "done": [K, N]} (single-env states: without the N axis)."""
+        self._flush()
         single = _single_of(state)
         n, D, K = self.num_envs, self.observation_size, int(nsteps)
         if K < 1:
@@ -755,6 +799,7 @@ class PupperV3Env:
     def holds(self, state: State) -> bool:
         """The device buffers hold exactly `state`: the last state this env issued, unedited, and
         no launch or upload since."""
+        self._flush()  # (a queued step's state is held once its launch is issued)
         return (isinstance(state, DeviceState) and state.__dict__.get("_env") is self and state._gen == self._gen
                 and state.unedited())
 
@@ -763,12 +808,13 @@ class PupperV3Env:
         return ((_abi.F_STATE, _abi.F_METRICS) + ((_abi.F_PIPELINE,) if self._pipeline_output else ())
                 + tuple(self._lazy_extra))
 
-    def _download(self, field_id: int, src_dev: Optional[int] = None) -> np.ndarray:
+    def _download(self, field_id: int, src_dev: Optional[int] = None, raw: bool = False) -> np.ndarray:
         if src_dev is None:
-            return self._get(field_id)
+            return self._get(field_id, raw=raw)
         n = self._field_elems[field_id]
         out = np.empty((self.num_envs, n), dtype=np.float32)
-        _lib.check(self._L.pp3_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(src_dev), out.nbytes))
+        _lib.check((self._raw if raw else self._L).pp3_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(src_dev),
+                                                                 out.nbytes))
         return out
 
     def _output_views(self, lease, single: bool):
@@ -813,6 +859,7 @@ class PupperV3Env:
         """Called before anything changes the device buffers: the last issued state, if still alive
         and not yet downloaded, gets a device-side snapshot of its lazy fields (d2d copies on the
         env's stream, ordered before the launch), then the buffers' generation advances."""
+        self._flush()  # a queued step launches first (its state is the one this launch overwrites)
         st = self._issued() if self._issued is not None else None
         if st is not None and not st.materialized and st._snap is None and st._gen == self._gen:
             buf = self._snap_pool.pop() if self._snap_pool else _lib.DeviceBuffer(self._snap_bytes, self.device)
@@ -822,6 +869,7 @@ class PupperV3Env:
                 _lib.check(self._L.pp3_memcpy_d2d(C.c_void_p(buf.ptr.value + self._snap_offsets[f]), C.c_void_p(ptr),
                                                   self.num_envs * n * 4, C.c_void_p(stream)))
             st.__dict__["_snap"] = buf
+            self._n_snapshots += 1
             weakref.finalize(st, _return_snapshot, self._snap_pool, st.__dict__)
         self._gen += 1
 
@@ -923,12 +971,33 @@ def _single_of(state) -> bool:
     return np.ndim(state.reward) == 0
 
 
+class _FlushingLib:
+    """The library as PupperV3Env._L: each call first issues the env's queued step() launch
+    (DEFER_LAUNCH), so whatever reads or changes the device sees the state step() returned."""
+
+    def __init__(self, env: "PupperV3Env", lib):
+        self._env = weakref.ref(env)
+        self._lib = lib
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        env_ref = self._env
+
+        def call(*args):
+            env = env_ref()
+            if env is not None and env.__dict__.get("_pending") is not None:
+                env._flush()
+            return fn(*args)
+        call.__name__ = name
+        return call
+
+
 class _ActSlot:
     """One page-locked action staging block of PupperV3Env.step's ring and the completion event of
     the last launch that read it (pp3_event_*)."""
 
     def __init__(self, env: "PupperV3Env", nbytes: int):
-        self._L = env._L
+        self._L = getattr(env, "_raw", None) or env._L  # (events never wait for a queued step launch)
         self._h = env._h
         self.block = _lib.PinnedBlock(nbytes)
         self.arr = np.asarray(self.block)

@@ -190,6 +190,8 @@ class Comm:
 
     def gather(self, env, nmax: int, dst_dev: Optional[int], root: int = 0, stream: Optional[int] = None) -> None:
         """Learner batch of every rank's shard into dst_dev (see module doc); root < 0 = all-gather."""
+        if hasattr(env, "_flush"):
+            env._flush()  # a step() launch still queued (environment.DEFER_LAUNCH) first
         self._lib.check_comm(self._L.pp3_gather(self._h, env._h, int(nmax), int(root),
                                                 C.c_void_p(dst_dev) if dst_dev else None,
                                                 C.c_void_p(stream) if stream else None))

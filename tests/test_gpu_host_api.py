@@ -270,6 +270,43 @@ def test_async_steps_match_synchronous_steps(require_gpu, zero_copy):
         environment.ASYNC_STEP, environment.ACTIONS_ZERO_COPY = saved
 
 
+def test_deferred_step_loop_takes_no_snapshots(require_gpu):
+    """`state = env.step(state, action)` with DEFER_LAUNCH: each launch is issued at the next call,
+    after the caller has dropped the state it overwrites, so the loop takes no device snapshot and
+    ends bit for bit where the synchronous loop does; a state the caller keeps is still snapshotted
+    and reads its own record; reading a returned state's fields issues its launch."""
+    from pupperv3_mjx import environment
+    saved = environment.ASYNC_STEP, environment.DEFER_LAUNCH
+    acts = np.random.RandomState(12).uniform(-1, 1, size=(9, N, 12)).astype(np.float32)
+    try:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH = False, False
+        e = _env()
+        st = e.reset(make_keys(13, N))
+        recs = []
+        for t in range(9):
+            st = e.step(st, acts[t])
+            recs.append(np.array(st._record))
+        ref_obs = np.array(st.obs)
+        e.close()
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH = True, True
+        e = _env()
+        st = e.reset(make_keys(13, N))
+        for t in range(6):
+            st = e.step(st, acts[t])
+        assert e._n_snapshots == 0 and e._pending is not None
+        kept = st  # kept past the next two steps: snapshotted when the launch after it is issued
+        for t in range(6, 9):
+            st = e.step(st, acts[t])
+        assert e._n_snapshots == 1
+        np.testing.assert_array_equal(kept._record, recs[5])
+        np.testing.assert_array_equal(st.obs, ref_obs)  # (issues the last queued launch)
+        assert e._pending is None
+        np.testing.assert_array_equal(st._record, recs[8])
+        e.close()
+    finally:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH = saved
+
+
 def test_retired_pools_free_their_blocks(require_gpu):
     """A page-locked block leased from a pool the env has retired (a trajectory length no longer
     used, or a closed env) is freed when released, not parked in the orphaned pool (advisor r04)."""

@@ -28,13 +28,13 @@ for step in "$@"; do
       REPS=${REPS:-4} STEPS=20 bash tools/ab_bench.sh > $OUT/ab_driver.txt 2>&1 || { tail $OUT/ab_driver.txt; exit 1; }
       cat $OUT/ab_driver.txt ;;
     hostapi)
-      for mode in sync async async_zc sync async async_zc; do
+      for mode in sync async async_zc defer sync async async_zc defer; do
         for pipe in 1 0; do
           timeout -k 10 200 python tools/host_api_trace.py 200 $pipe $mode >> $OUT/host_api_plain.txt 2>&1 || { tail $OUT/host_api_plain.txt; exit 1; }
         done
       done
       cat $OUT/host_api_plain.txt
-      for mode in sync async; do
+      for mode in sync defer; do
         timeout -k 10 240 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/host_api_trace_$mode -o run --output-format csv -- python3 tools/host_api_trace.py 200 1 $mode > $OUT/host_api_trace_$mode.log 2>&1 || { tail $OUT/host_api_trace_$mode.log; exit 1; }
         grep "env.step" $OUT/host_api_trace_$mode.log
       done ;;

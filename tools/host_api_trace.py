@@ -2,12 +2,13 @@
 the host API's time per step goes).  4096 envs (bench.py workload), 20 untimed steps, then `N`
 timed env.step(state, numpy actions) calls; prints us/step.
 
-  python tools/host_api_trace.py [N] [pipeline_output 0|1] [sync|async|async_zc]
+  python tools/host_api_trace.py [N] [pipeline_output 0|1] [sync|async|async_zc|defer]
 
 Modes: sync = every step synchronises before it returns (the round-4 host API); async = step()
 returns at once, obs / reward / done wait for their own launch (environment.ASYNC_STEP); async_zc =
 async, and the launch reads the actions straight from the page-locked staging block
-(environment.ACTIONS_ZERO_COPY).
+(environment.ACTIONS_ZERO_COPY); defer = async_zc with each launch issued at the next call
+(environment.DEFER_LAUNCH: no device snapshot of the state the caller has dropped; the default).
 """
 import os
 import sys
@@ -24,9 +25,10 @@ from pupperv3_mjx.environment import PupperV3Env  # noqa: E402
 E = 4096
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 pipe = (sys.argv[2] == "1") if len(sys.argv) > 2 else True
-mode = sys.argv[3] if len(sys.argv) > 3 else "async"
+mode = sys.argv[3] if len(sys.argv) > 3 else "defer"
 environment.ASYNC_STEP = mode != "sync"
-environment.ACTIONS_ZERO_COPY = mode == "async_zc"
+environment.ACTIONS_ZERO_COPY = mode in ("async_zc", "defer")
+environment.DEFER_LAUNCH = mode == "defer"
 env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=pipe)
 acts = np.random.RandomState(3).uniform(-1, 1, size=(N + 20, E, 12)).astype(np.float32)
 st = env.reset(sharding.shard_keys(0, E, 1, 0))
