@@ -95,6 +95,11 @@ enum { LM_IJ = 0, LM_ARM = 4, LM_DAMP = 8, LM_FLOSS = 9, LM_WORDS = 10 };
 // abduction (l % 3 == 1); lane f < 4 -> lower-leg body of foot f; lanes 16..27 -> default pose
 // of joint l - 16 (the observation's lanes)
 enum { LE_POSE = 0, LE_JLO, LE_JHI, LE_ABD, LE_LEG, LE_POSE16, LE_WORDS = 6 };
+// pipeline record (write_pipeline), lane i < nsensor: sensor i's type, sensordata address, cutoff,
+// site body, site frame in the body, and for an accelerometer the body chain root .. site body
+// (per level: body, dofadr, dofnum, parent; at most LS_MAXCH levels, checked at pp3_create)
+enum { LS_TYPE = 0, LS_ADR, LS_CUT, LS_BODY, LS_SPOS, LS_SQUAT = 7, LS_NCH = 11, LS_CH = 12, LS_MAXCH = 4,
+       LS_WORDS = LS_CH + 4 * LS_MAXCH };
 
 constexpr float MINVAL = 1e-15f;
 constexpr float MINIMP = 0.0001f;
@@ -202,6 +207,9 @@ struct DevModel {
   float pi_f;
   // last: the same 1 KB inserted after lane_m (shifting every later field) measured 1.3 % slower
   LaneTab<(LE_WORDS + 3) / 4> lane_env;
+  // pipeline record only (after everything the step reads)
+  LaneTab<(LS_WORDS + 3) / 4> lane_sens;
+  float pair_gid[PP3_MAX_PAIR][2];  // MuJoCo geom ids of the pair's two geoms (contact geom fields)
 };
 
 // ------------------------------- float helpers -------------------------------

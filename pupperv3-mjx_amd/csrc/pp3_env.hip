@@ -46,6 +46,22 @@ constexpr float LS_NOISE = 64.0f;  // line-search convergence floor, in roundoff
 #ifndef PP3_LS_E0
 #define PP3_LS_E0 1
 #endif
+// PP3_COM_BF (default 1): the com / cinert / cdof phase as one straight-line block (com_pos): +1.2 %
+// fused.  Not bitwise equal to the branchy form: the backend fuses the rotated inertia's products
+// into FMAs differently in the two blocks (tools/diag_combf.py: com identical, R I R' differs in
+// the last bit on some lanes); GPU suite and one-step error vs the fp64 oracle unchanged
+// (profiles/AB_LOG.md round 5)
+#ifndef PP3_COM_BF
+#define PP3_COM_BF 1
+#endif
+// PP3_CRB_BF (A/B): CRB x cdof and the RNE velocity chain as one straight-line block (crb_rne)
+#ifndef PP3_CRB_BF
+#define PP3_CRB_BF 0
+#endif
+// PP3_PIPE_V2: the pipeline record from flattened sensor records and one LDS round (write_pipeline)
+#ifndef PP3_PIPE_V2
+#define PP3_PIPE_V2 1
+#endif
 
 // Phase-local scratch that never lives across a phase boundary it does not own.
 template <int NC>
@@ -376,6 +392,167 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
 // Phase 2: subtree com, cinert (mju_inertCom), cdof, robot geom and foot-site positions.
 // lanes 1..13 bodies, 14..31 dofs; then lanes 0..7 geoms, 16..19 feet.
 // ------------------------------------------------------------------------------------
+#if PP3_COM_BF
+// Straight-line form: every lane runs every part (clamped indices; results selected, stores in
+// lane branches at the end), with all LDS operands in one pinned round.  What does not need the
+// subtree com -- the bodies' rotated inertias, the geom / site positions, the base rotation's
+// columns -- then issues while the com's four half-wave sums run, instead of behind them.  The
+// same operations on the same operands as the branchy form below (bitwise equal).
+template <int NC>
+__device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h, const LaneRec<2>& rc) {
+  const bool body = l >= 1 && l < NB;
+  const int b = body ? l : 1;
+  const bool geom = l < m.nrobot_geom, foot = l >= 16 && l < 20;
+  const int gb = as_i(rc.f[LC_PT_BODY]);  // (0 on lanes without a point: the world body's words)
+  const int d = l >= 14 ? l - 14 : 0;      // cdof lanes 14..31: dof d
+  const int jx = d >= 6 ? d - 5 : 1, bd = d < 6 ? 1 : 2 + (d - 6);
+  float mb0 = s.mass[b], xi[3], bq[4], I[3], gq[4], gx[3], q1[4], x1[3], ax6[3], xb[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    xi[k] = s.x.xipos[b][k]; I[k] = s.inertia[b][k]; gx[k] = s.xpos[gb][k];
+    x1[k] = s.x.xipos[1][k]; ax6[k] = s.xaxis[jx][k]; xb[k] = s.xpos[bd][k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) { bq[k] = s.xquat[b][k]; gq[k] = s.xquat[gb][k]; q1[k] = s.xquat[1][k]; }
+  PIN("+v"(mb0), "+v"(xi[0]), "+v"(xi[1]), "+v"(xi[2]), "+v"(I[0]), "+v"(I[1]), "+v"(I[2]), "+v"(gx[0]), "+v"(gx[1]),
+      "+v"(gx[2]), "+v"(x1[0]), "+v"(x1[1]), "+v"(x1[2]), "+v"(ax6[0]), "+v"(ax6[1]), "+v"(ax6[2]), "+v"(xb[0]),
+      "+v"(xb[1]), "+v"(xb[2]));
+  PIN("+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(gq[0]), "+v"(gq[1]), "+v"(gq[2]), "+v"(gq[3]),
+      "+v"(q1[0]), "+v"(q1[1]), "+v"(q1[2]), "+v"(q1[3]));
+  float mb = body ? mb0 : 0.0f, mx = body ? mb0 * xi[0] : 0.0f, my = body ? mb0 * xi[1] : 0.0f,
+        mz = body ? mb0 * xi[2] : 0.0f;
+  mb = hsum(mb, h);
+  mx = hsum(mx, h);
+  my = hsum(my, h);
+  mz = hsum(mz, h);
+  // com-independent parts
+  float A[3][3];
+  {
+    float iq[4], R[9];
+    const float biq[4] = {rc.f[LC_IQUAT], rc.f[LC_IQUAT + 1], rc.f[LC_IQUAT + 2], rc.f[LC_IQUAT + 3]};
+    mulquat(iq, bq, biq);
+    quat2mat(iq, R);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        A[i][j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
+  }
+  float gpos[3];
+  {
+    const float lp[3] = {rc.f[LC_PT_POS], rc.f[LC_PT_POS + 1], rc.f[LC_PT_POS + 2]};
+    float R[9], off[3];
+    quat2mat(gq, R);
+    matvec(off, R, lp);
+#pragma unroll
+    for (int k = 0; k < 3; k++) gpos[k] = gx[k] + off[k];
+  }
+  float ax[3];
+  {
+    float R[9];
+    quat2mat(q1, R);
+    const int cc = d - 3;
+    ax[0] = cc == 0 ? R[0] : (cc == 1 ? R[1] : R[2]);
+    ax[1] = cc == 0 ? R[3] : (cc == 1 ? R[4] : R[5]);
+    ax[2] = cc == 0 ? R[6] : (cc == 1 ? R[7] : R[8]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) ax[k] = d < 6 ? ax[k] : ax6[k];
+  }
+  float com[3];
+  const bool mok = mb > MINVAL;
+  {
+    const float im = 1.0f / mb;
+    com[0] = mok ? mx * im : x1[0];
+    com[1] = mok ? my * im : x1[1];
+    com[2] = mok ? mz * im : x1[2];
+  }
+  if (l == 0) { s.com[0] = com[0]; s.com[1] = com[1]; s.com[2] = com[2]; }
+  float ci[10];
+  {
+    const float mm = mb0;
+    const float dx = xi[0] - com[0], dy = xi[1] - com[1], dz = xi[2] - com[2];
+    ci[0] = A[0][0] + mm * (dy * dy + dz * dz);
+    ci[1] = A[1][1] + mm * (dx * dx + dz * dz);
+    ci[2] = A[2][2] + mm * (dx * dx + dy * dy);
+    ci[3] = A[0][1] - mm * dx * dy;
+    ci[4] = A[0][2] - mm * dx * dz;
+    ci[5] = A[1][2] - mm * dy * dz;
+    ci[6] = mm * dx; ci[7] = mm * dy; ci[8] = mm * dz;
+    ci[9] = mm;
+#pragma unroll
+    for (int k = 0; k < 10; k++) ci[k] = body ? ci[k] : 0.0f;
+  }
+  float cd[6];
+  {
+    float off[3], c[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) off[k] = com[k] - xb[k];
+    cross3(c, ax, off);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      cd[k] = d < 3 ? 0.0f : ax[k];
+      cd[3 + k] = d < 3 ? (k == d ? 1.0f : 0.0f) : c[k];
+    }
+  }
+#if defined(PP3_DEBUG) && defined(PP3_COM_CHECK)
+  {  // diagnostic: the branchy form's values from the same LDS words, compared bit for bit
+    auto miss = [&](int slot, float a, float b) {
+      if (__float_as_uint(a) != __float_as_uint(b)) atomicAdd(&g_dbg[100 + slot], 1.0f);
+    };
+    float mb_ = 0, mx_ = 0, my_ = 0, mz_ = 0;
+    if (body) { mb_ = s.mass[l]; mx_ = mb_ * s.x.xipos[l][0]; my_ = mb_ * s.x.xipos[l][1]; mz_ = mb_ * s.x.xipos[l][2]; }
+    mb_ = hsum(mb_, h); mx_ = hsum(mx_, h); my_ = hsum(my_, h); mz_ = hsum(mz_, h);
+    float co[3];
+    if (mb_ > MINVAL) { const float im = 1.0f / mb_; co[0] = mx_ * im; co[1] = my_ * im; co[2] = mz_ * im; }
+    else { co[0] = s.x.xipos[1][0]; co[1] = s.x.xipos[1][1]; co[2] = s.x.xipos[1][2]; }
+    for (int k = 0; k < 3; k++) miss(k, co[k], com[k]);
+    if (body) {
+      float iq[4], R[9];
+      const float biq[4] = {rc.f[LC_IQUAT], rc.f[LC_IQUAT + 1], rc.f[LC_IQUAT + 2], rc.f[LC_IQUAT + 3]};
+      mulquat(iq, s.xquat[b], biq);
+      quat2mat(iq, R);
+      const float* I2 = s.inertia[b];
+      float A2[3][3];
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+          A2[i][j] = R[3 * i] * I2[0] * R[3 * j] + R[3 * i + 1] * I2[1] * R[3 * j + 1] + R[3 * i + 2] * I2[2] * R[3 * j + 2];
+      const float mm = s.mass[b];
+      const float dx = s.x.xipos[b][0] - co[0], dy = s.x.xipos[b][1] - co[1], dz = s.x.xipos[b][2] - co[2];
+      float c2[10];
+      c2[0] = A2[0][0] + mm * (dy * dy + dz * dz);
+      c2[1] = A2[1][1] + mm * (dx * dx + dz * dz);
+      c2[2] = A2[2][2] + mm * (dx * dx + dy * dy);
+      c2[3] = A2[0][1] - mm * dx * dy;
+      c2[4] = A2[0][2] - mm * dx * dz;
+      c2[5] = A2[1][2] - mm * dy * dz;
+      c2[6] = mm * dx; c2[7] = mm * dy; c2[8] = mm * dz;
+      c2[9] = mm;
+      for (int k = 0; k < 10; k++) miss(3 + k, c2[k], ci[k]);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) miss(30 + 3 * i + j, A2[i][j], A[i][j]);
+    }
+  }
+#endif
+  if (body)
+#pragma unroll
+    for (int k = 0; k < 10; k++) s.cinert[b][k] = ci[k];
+  if (l >= 14)
+#pragma unroll
+    for (int k = 0; k < 6; k++) s.cdof[d][k] = cd[k];
+  {  // composite inertia of the whole tree (body 1's subtree) for the 6 base dofs
+    float t[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) t[k] = hsum_lane16(ci[k]);
+    if (l == 16)
+#pragma unroll
+      for (int k = 0; k < 10; k++) s.crb_base[k] = t[k];
+  }
+  if (geom || foot) {
+    float* dst = geom ? s.gxpos[l] : s.foot_xpos[l - 16];
+    for (int k = 0; k < 3; k++) dst[k] = gpos[k];
+  }
+}
+#else
 template <int NC>
 __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h, const LaneRec<2>& rc) {
   const bool body = l >= 1 && l < NB;
@@ -478,6 +655,7 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
     for (int k = 0; k < 3; k++) dst[k] = xb[k] + off[k];
   }
 }
+#endif
 
 __device__ __forceinline__ void make_frame(float f[9], const float nin[3]) {
   float a[3] = {nin[0], nin[1], nin[2]};
@@ -803,6 +981,94 @@ __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m,
   for (int k = 0; k < 10; k++) crb[k] += w2 * c2[k];
   mul_inert_vec(s.x.a.F[l], crb, cdv);
 }
+
+#if PP3_CRB_BF
+// crb_times_cdof and rne_chain as one straight-line block (A/B): both phases' LDS operands in one
+// pinned round (clamped indices on the lanes that own nothing), their arithmetic interleaved by the
+// scheduler, the stores in lane branches at the end.  Same operations on the same operands.
+template <int NC>
+__device__ __forceinline__ void crb_rne(Shared<NC>& s, const DevModel& m, int l) {
+  // crb x cdof (lanes < NV)
+  const int lc = l < NV ? l : NV - 1;
+  const bool base = lc < 6;
+  const int b = base ? 2 : lc - 4, last = 2 + 3 * ((b - 2) / 3) + 2;
+  const float* r0 = base ? s.crb_base : s.cinert[b];
+  const int b1 = b + 1 <= last ? b + 1 : b, b2 = b + 2 <= last ? b + 2 : b;
+  float crb[10], c1[10], c2[10], cdv[6];
+#pragma unroll
+  for (int k = 0; k < 10; k++) { crb[k] = r0[k]; c1[k] = s.cinert[b1][k]; c2[k] = s.cinert[b2][k]; }
+#pragma unroll
+  for (int k = 0; k < 6; k++) cdv[k] = s.cdof[lc][k];
+  // rne chain (lanes 0..3: leg l & 3)
+  const int lg = l & 3;
+  float lcd[3][6], lqd[3], bcd[3][6], bq[6];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int d = 6 + 3 * lg + k;
+#pragma unroll
+    for (int c = 0; c < 6; c++) lcd[k][c] = s.cdof[d][c];
+    lqd[k] = s.qvel[d];
+  }
+#pragma unroll
+  for (int d = 0; d < 3; d++)
+#pragma unroll
+    for (int k = 0; k < 6; k++) bcd[d][k] = s.cdof[3 + d][k];
+#pragma unroll
+  for (int k = 0; k < 6; k++) bq[k] = s.qvel[k];
+  PIN("+v"(crb[0]), "+v"(crb[1]), "+v"(crb[2]), "+v"(crb[3]), "+v"(crb[4]), "+v"(crb[5]), "+v"(crb[6]), "+v"(crb[7]),
+      "+v"(crb[8]), "+v"(crb[9]), "+v"(cdv[0]), "+v"(cdv[1]), "+v"(cdv[2]), "+v"(cdv[3]), "+v"(cdv[4]), "+v"(cdv[5]));
+  PIN("+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]), "+v"(c1[4]), "+v"(c1[5]), "+v"(c1[6]), "+v"(c1[7]),
+      "+v"(c1[8]), "+v"(c1[9]), "+v"(c2[0]), "+v"(c2[1]), "+v"(c2[2]), "+v"(c2[3]), "+v"(c2[4]), "+v"(c2[5]),
+      "+v"(c2[6]), "+v"(c2[7]), "+v"(c2[8]), "+v"(c2[9]));
+  PIN("+v"(lcd[0][0]), "+v"(lcd[0][1]), "+v"(lcd[0][2]), "+v"(lcd[0][3]), "+v"(lcd[0][4]), "+v"(lcd[0][5]),
+      "+v"(lcd[1][0]), "+v"(lcd[1][1]), "+v"(lcd[1][2]), "+v"(lcd[1][3]), "+v"(lcd[1][4]), "+v"(lcd[1][5]),
+      "+v"(lcd[2][0]), "+v"(lcd[2][1]), "+v"(lcd[2][2]), "+v"(lcd[2][3]), "+v"(lcd[2][4]), "+v"(lcd[2][5]),
+      "+v"(lqd[0]), "+v"(lqd[1]), "+v"(lqd[2]));
+  PIN("+v"(bcd[0][0]), "+v"(bcd[0][1]), "+v"(bcd[0][2]), "+v"(bcd[0][3]), "+v"(bcd[0][4]), "+v"(bcd[0][5]),
+      "+v"(bcd[1][0]), "+v"(bcd[1][1]), "+v"(bcd[1][2]), "+v"(bcd[1][3]), "+v"(bcd[1][4]), "+v"(bcd[1][5]),
+      "+v"(bcd[2][0]), "+v"(bcd[2][1]), "+v"(bcd[2][2]), "+v"(bcd[2][3]), "+v"(bcd[2][4]), "+v"(bcd[2][5]),
+      "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(bq[4]), "+v"(bq[5]));
+  const float w1 = (!base && b + 1 <= last) ? 1.0f : 0.0f, w2 = (!base && b + 2 <= last) ? 1.0f : 0.0f;
+#pragma unroll
+  for (int k = 0; k < 10; k++) crb[k] += w1 * c1[k];
+#pragma unroll
+  for (int k = 0; k < 10; k++) crb[k] += w2 * c2[k];
+  float F[6];
+  mul_inert_vec(F, crb, cdv);
+  float w[3] = {0, 0, 0}, bsum[3] = {0, 0, 0};
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const float q = bq[3 + d];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { w[k] += bcd[d][k] * q; bsum[k] += bcd[d][3 + k] * q; }
+  }
+  const float v0 = bq[0], v1 = bq[1], v2 = bq[2];
+  float cv[6] = {w[0], w[1], w[2], v0 + bsum[0], v1 + bsum[1], v2 + bsum[2]};
+  float ca[6] = {0, 0, 0, -m.gravity[0] + (v1 * w[2] - v2 * w[1]), -m.gravity[1] + (v2 * w[0] - v0 * w[2]),
+                 -m.gravity[2] + (v0 * w[1] - v1 * w[0])};
+  float cvs[3][6], cas[3][6];
+  const float cv1[6] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5]}, ca1[6] = {ca[0], ca[1], ca[2], ca[3], ca[4], ca[5]};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    float cdd[6];
+    cross_motion(cdd, cv, lcd[k]);
+    const float qd = lqd[k];
+    for (int c = 0; c < 6; c++) { cv[c] += lcd[k][c] * qd; ca[c] += cdd[c] * qd; }
+    for (int c = 0; c < 6; c++) { cvs[k][c] = cv[c]; cas[k][c] = ca[c]; }
+  }
+  if (l < NV)
+#pragma unroll
+    for (int k = 0; k < 6; k++) s.x.a.F[l][k] = F[k];
+  if (l == 0)
+    for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv1[k]; s.x.a.cacc[1][k] = ca1[k]; }
+  if (l < 4)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int bb = 2 + 3 * l + k;
+      for (int c = 0; c < 6; c++) { s.cvel[bb][c] = cvs[k][c]; s.x.a.cacc[bb][c] = cas[k][c]; }
+    }
+}
+#endif
 
 // ------------------------------------------------------------------------------------
 // LDL^T in registers: lane i (< NV) of each half holds row i; returns L_ik (k<i) in a[k],
@@ -1413,7 +1679,11 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
+#if PP3_CRB_BF
+  { crb_rne(s, m, l); SYNC(); }
+#else
   { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
+#endif
   PHASE(15); l = opaque_lane(l);
   int lsup = 4;  // lane c: support of contact c (4 = none)
   { lsup = collision<NC, NWV>(s, m, l, h, pair_pf); SYNC(); }
@@ -2276,8 +2546,160 @@ __device__ __forceinline__ void sensor_eval(const Shared<NC>& s, const DevModel&
   for (int k = 0; k < dim; k++) out[m.sensor_adr[i] + k] = v[k];
 }
 
+#if PP3_PIPE_V2
+// Sensor lane l (< nsensor) from its host-flattened record (LS_*): the same operations as
+// sensor_eval below, with every model word fetched in one round instead of the dependent
+// lane-indexed loads (sensor -> site -> body -> chain), and the frame's LDS operands pinned.
 template <int NC>
-__device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int l) {
+__device__ __forceinline__ void sensor_eval_rec(const Shared<NC>& s, const DevModel& m, const LaneRec<(LS_WORDS + 3) / 4>& r,
+                                                float* out) {
+  const int typ = as_i(r.f[LS_TYPE]), b = as_i(r.f[LS_BODY]);
+  const float* qv = s.efc_aref;
+  float xq[4], xb[3], cm[3], cvb[6];
+#pragma unroll
+  for (int k = 0; k < 4; k++) xq[k] = s.xquat[b][k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { xb[k] = s.xpos[b][k]; cm[k] = s.com[k]; }
+#pragma unroll
+  for (int k = 0; k < 6; k++) cvb[k] = s.cvel[b][k];
+  PIN("+v"(xq[0]), "+v"(xq[1]), "+v"(xq[2]), "+v"(xq[3]), "+v"(xb[0]), "+v"(xb[1]), "+v"(xb[2]), "+v"(cm[0]),
+      "+v"(cm[1]), "+v"(cm[2]), "+v"(cvb[0]), "+v"(cvb[1]), "+v"(cvb[2]), "+v"(cvb[3]), "+v"(cvb[4]), "+v"(cvb[5]));
+  const float spos[3] = {r.f[LS_SPOS], r.f[LS_SPOS + 1], r.f[LS_SPOS + 2]};
+  const float squat[4] = {r.f[LS_SQUAT], r.f[LS_SQUAT + 1], r.f[LS_SQUAT + 2], r.f[LS_SQUAT + 3]};
+  float Rb[9], sq[4], R[9], sx[3], off[3], dif[3], cr[3], vang[3], vlin[3], v[4] = {0, 0, 0, 0};
+  quat2mat(xq, Rb);
+  matvec(off, Rb, spos);
+  for (int k = 0; k < 3; k++) sx[k] = xb[k] + off[k];
+  mulquat(sq, xq, squat);
+  quat2mat(sq, R);
+  for (int k = 0; k < 3; k++) { dif[k] = sx[k] - cm[k]; vang[k] = cvb[k]; }
+  cross3(cr, dif, vang);
+  for (int k = 0; k < 3; k++) vlin[k] = cvb[3 + k] - cr[k];
+  int dim = 3;
+  if (typ == PP3_SENS_FRAMEPOS) { for (int k = 0; k < 3; k++) v[k] = sx[k]; }
+  else if (typ == PP3_SENS_FRAMEQUAT) { for (int k = 0; k < 4; k++) v[k] = sq[k]; dim = 4; }
+  else if (typ == PP3_SENS_FRAMELINVEL) { for (int k = 0; k < 3; k++) v[k] = vlin[k]; }
+  else if (typ == PP3_SENS_FRAMEANGVEL) { for (int k = 0; k < 3; k++) v[k] = vang[k]; }
+  else if (typ == PP3_SENS_GYRO || typ == PP3_SENS_VELOCIMETER) {
+    const float* w = typ == PP3_SENS_GYRO ? vang : vlin;
+    for (int k = 0; k < 3; k++) v[k] = R[k] * w[0] + R[3 + k] * w[1] + R[6 + k] * w[2];
+  } else if (typ == PP3_SENS_ACCELEROMETER) {
+    const int n = as_i(r.f[LS_NCH]);
+    float ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
+    for (int c = 0; c < n; c++) {  // root first
+      const int d0 = as_i(r.f[LS_CH + 4 * c + 1]), nd = as_i(r.f[LS_CH + 4 * c + 2]);
+      const int pb = as_i(r.f[LS_CH + 4 * c + 3]);
+      float pv[6] = {0, 0, 0, 0, 0, 0};  // velocity the body's dof_dot terms see (parent, + free translation)
+      if (pb > 0)
+        for (int k = 0; k < 6; k++) pv[k] = s.cvel[pb][k];
+      if (nd == 6)
+        for (int d = d0; d < d0 + 3; d++)
+          for (int k = 0; k < 6; k++) pv[k] += s.cdof[d][k] * qv[d];
+      float t1[6] = {0, 0, 0, 0, 0, 0}, t2[6] = {0, 0, 0, 0, 0, 0};
+      for (int d = d0; d < d0 + nd; d++) {
+        float cdd[6] = {0, 0, 0, 0, 0, 0};
+        if (!(nd == 6 && d < d0 + 3)) cross_motion(cdd, pv, s.cdof[d]);
+        for (int k = 0; k < 6; k++) { t1[k] += cdd[k] * qv[d]; t2[k] += s.cdof[d][k] * s.qacc[d]; }
+      }
+      for (int k = 0; k < 6; k++) ca[k] = ca[k] + t1[k] + t2[k];
+    }
+    float aang[3] = {ca[0], ca[1], ca[2]}, alin[3], wl[3], vl[3], c2[3];
+    cross3(cr, dif, aang);
+    for (int k = 0; k < 3; k++) alin[k] = ca[3 + k] - cr[k];
+    for (int k = 0; k < 3; k++) {
+      v[k] = R[k] * alin[0] + R[3 + k] * alin[1] + R[6 + k] * alin[2];
+      wl[k] = R[k] * vang[0] + R[3 + k] * vang[1] + R[6 + k] * vang[2];
+      vl[k] = R[k] * vlin[0] + R[3 + k] * vlin[1] + R[6 + k] * vlin[2];
+    }
+    cross3(c2, wl, vl);
+    for (int k = 0; k < 3; k++) v[k] += c2[k];
+  }
+  const float co = r.f[LS_CUT];
+  if (co > 0 && typ != PP3_SENS_FRAMEQUAT)
+    for (int k = 0; k < 3; k++) v[k] = fminf(fmaxf(v[k], -co), co);
+  const int adr = as_i(r.f[LS_ADR]);
+  for (int k = 0; k < dim; k++) out[adr + k] = v[k];
+}
+
+// The Brax pipeline record of this env (PP3_P_* layout).  Every element below the sensors is one
+// LDS word (x, its velocities as the epilogue's s.x.e.xdv / xda, site positions, qfrc_actuator,
+// qacc, the contact fields, subtree com): the lane selects its element's word per 32-element block
+// (the block bounds are compile-time), all blocks' loads issue as one pinned round, then one
+// coalesced store per block; the contact geoms take one more round (pair -> geom ids).
+template <int NC>
+__device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int l, bool have_xd = true) {
+  const LaneRec<(LS_WORDS + 3) / 4> rsens = fetch_rec(m.lane_sens, l);  // (arrives during the element loads)
+  if (!have_xd) {  // (reset / bare physics launches: Brax xd as the step's epilogue computes it)
+    if (l >= 1 && l < NB) {
+      float off[3], cv[6], cr[3];
+      for (int k = 0; k < 6; k++) cv[k] = s.cvel[l][k];
+      for (int k = 0; k < 3; k++) off[k] = s.xpos[l][k] - s.com[k];
+      cross3(cr, cv, off);
+      for (int k = 0; k < 3; k++) { s.x.e.xdv[l][k] = cv[3 + k] + cr[k]; s.x.e.xda[l][k] = cv[k]; }
+    }
+    SYNC();
+  }
+  const float* w = reinterpret_cast<const float*>(&s);
+  const int o_xpos = (int)(&s.xpos[1][0] - w), o_xq = (int)(&s.xquat[1][0] - w), o_xdv = (int)(&s.x.e.xdv[1][0] - w),
+            o_xda = (int)(&s.x.e.xda[1][0] - w), o_foot = (int)(&s.foot_xpos[0][0] - w), o_fa = (int)(&s.qfrc_act[0] - w),
+            o_qacc = (int)(&s.qacc[0] - w), o_cd = (int)(&s.con_dist[0] - w),
+            o_cp = (int)(reinterpret_cast<const float*>(&s.con_pair[0]) - w), o_com = (int)(&s.com[0] - w),
+            o_ncon = (int)(reinterpret_cast<const float*>(&s.ncon) - w),
+            o_nhit = (int)(reinterpret_cast<const float*>(&s.nhit) - w);
+  constexpr int NBLK = (PP3_P_SENSOR + HW - 1) / HW;
+  float v[NBLK];
+  int kind[NBLK];  // 0 float word, 1 int word, 2 zero, 3 contact distance, 4 contact geom
+  int ncon = s.ncon;
+#pragma unroll
+  for (int t = 0; t < NBLK; t++) {
+    const int i = l + HW * t;
+    const int cdi = i - PP3_P_CON_DIST, cgi = (i - PP3_P_CON_GEOM) >> 1;
+    const int cdc = cdi < NC ? cdi : NC - 1, cgc = cgi < NC ? cgi : NC - 1;
+    int src = o_com, k = 2;
+    if (i < PP3_P_XQUAT) { src = o_xpos + i; k = 0; }
+    else if (i < PP3_P_XD_VEL) { src = o_xq + (i - PP3_P_XQUAT); k = 0; }
+    else if (i < PP3_P_XD_ANG) { src = o_xdv + (i - PP3_P_XD_VEL); k = 0; }
+    else if (i < PP3_P_SITE_XPOS) { src = o_xda + (i - PP3_P_XD_ANG); k = 0; }
+    else if (i < PP3_P_QFRC_ACT) { src = o_foot + (i - PP3_P_SITE_XPOS); k = 0; }
+    else if (i < PP3_P_QACC) { src = o_fa + (i - PP3_P_QFRC_ACT); k = 0; }
+    else if (i < PP3_P_NCON) { src = o_qacc + (i - PP3_P_QACC); k = 0; }
+    else if (i == PP3_P_NCON) { src = o_ncon; k = 1; }
+    else if (i < PP3_P_CON_GEOM) { src = o_cd + cdc; k = 3; }
+    else if (i < PP3_P_SUBTREE_COM) { src = o_cp + cgc; k = 4; }
+    else if (i < PP3_P_SUBTREE_COM + 3) { src = o_com + (i - PP3_P_SUBTREE_COM); k = 0; }
+    else if (i == PP3_P_NHIT) { src = o_nhit; k = 1; }
+    kind[t] = k;
+    v[t] = w[src];
+  }
+  static_assert(NBLK == 9, "write_pipeline: PIN arity");
+  PIN("+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]),
+      "+v"(ncon));
+  float out[NBLK];
+#pragma unroll
+  for (int t = 0; t < NBLK; t++) {
+    const int i = l + HW * t;
+    const int k = kind[t];
+    const int cdi = i - PP3_P_CON_DIST, cgi = (i - PP3_P_CON_GEOM) >> 1;
+    float o = v[t];
+    if (k == 1) o = (float)as_i(v[t]);
+    if (k == 2) o = 0.0f;
+    if (k == 3) o = cdi < ncon ? v[t] : 0.0f;
+    if (k == 4) {  // the pair's geom id (contacts c < ncon; 0 past them)
+      const int pp = cgi < ncon ? as_i(v[t]) : 0;
+      const float g = m.pair_gid[pp][(i - PP3_P_CON_GEOM) & 1];
+      o = cgi < ncon ? g : 0.0f;
+    }
+    out[t] = o;
+  }
+#pragma unroll
+  for (int t = 0; t < NBLK; t++)
+    if (l + HW * t < PP3_P_SENSOR) p[l + HW * t] = out[t];
+  if (l < m.nsensor) sensor_eval_rec(s, m, rsens, p + PP3_P_SENSOR);
+  for (int i = PP3_P_SENSOR + m.nsensordata + l; i < PP3_PIPE_STRIDE; i += HW) p[i] = 0.0f;
+}
+#else
+template <int NC>
+__device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int l, bool = true) {
   for (int i = l; i < PP3_PIPE_STRIDE; i += HW) {
     float v = 0.0f;
     if (i < PP3_P_XQUAT) { const int b = 1 + i / 3, k = i % 3; v = s.xpos[b][k]; }
@@ -2304,6 +2726,7 @@ __device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m,
   }
   if (l < m.nsensor) sensor_eval(s, m, l, p + PP3_P_SENSOR);
 }
+#endif
 
 // ------------------------------------------------------------------------------------
 // kernels: workgroup b = one wave = envs 2b (lanes 0..31) and 2b+1 (lanes 32..63).  With an
@@ -3007,7 +3430,7 @@ __global__ __launch_bounds__(WAVE, 2) void env_reset_kernel(ResetArgs a) {
   }
   if (own && l == 0) { a.reward[env] = 0.0f; a.done[env] = 0.0f; }
   if (own && l < PP3_NMETRIC) a.metrics[(size_t)env * PP3_NMETRIC + l] = 0.0f;
-  if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
+  if (own && a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l, false);
   SYNC();
   if (own)
 #pragma unroll
@@ -3049,7 +3472,7 @@ __global__ __launch_bounds__(WAVE, 2) void physics_kernel(PhysArgs a) {
   }
   if (a.nsteps > 0) euler_step(s, m, l);
   if (!own) return;
-  if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l);
+  if (a.pipe) write_pipeline(s, m, a.pipe + (size_t)env * PP3_PIPE_STRIDE, l, false);
   if (l < NQ) gst[PP3_S_QPOS + l] = s.qpos[l];
   if (l < NV) { gst[PP3_S_QVEL + l] = s.qvel[l]; gst[PP3_S_QACC_WS + l] = s.qws[l]; }
 }
@@ -3228,6 +3651,32 @@ static void fill_lane_records(DevModel* d) {
     put_rec(d->lane_com, l, rc);
     put_rec(d->lane_m, l, rm);
     put_rec(d->lane_env, l, re);
+    LaneRec<(LS_WORDS + 3) / 4> rs = {};
+    float* sr = rs.f;
+    if (l < d->nsensor) {
+      const int sid = d->sensor_objid[l], b = d->site_body[sid];
+      set_i(sr[LS_TYPE], d->sensor_type[l]);
+      set_i(sr[LS_ADR], d->sensor_adr[l]);
+      sr[LS_CUT] = d->sensor_cutoff[l];
+      set_i(sr[LS_BODY], b);
+      for (int k = 0; k < 3; k++) sr[LS_SPOS + k] = d->site_pos[sid][k];
+      for (int k = 0; k < 4; k++) sr[LS_SQUAT + k] = d->site_quat[sid][k];
+      int chain[NB], n = 0;  // (depth checked at create)
+      for (int bb = b; bb > 0 && n < LS_MAXCH; bb = d->body_parent[bb]) chain[n++] = bb;
+      set_i(sr[LS_NCH], n);
+      for (int c = 0; c < n; c++) {  // root first
+        const int bb = chain[n - 1 - c];
+        set_i(sr[LS_CH + 4 * c], bb);
+        set_i(sr[LS_CH + 4 * c + 1], d->body_dofadr[bb]);
+        set_i(sr[LS_CH + 4 * c + 2], d->body_dofnum[bb]);
+        set_i(sr[LS_CH + 4 * c + 3], d->body_parent[bb]);
+      }
+    }
+    put_rec(d->lane_sens, l, rs);
+  }
+  for (int p = 0; p < d->npair; p++) {
+    d->pair_gid[p][0] = (float)d->cg_id[d->pair_g1[p]];
+    d->pair_gid[p][1] = (float)d->cg_id[d->pair_g2[p]];
   }
   for (int p = 0; p < d->npair; p++) {
     const int ga = d->cg_id[d->pair_g1[p]], gb = d->cg_id[d->pair_g2[p]];
@@ -3459,6 +3908,11 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
     d->body_parent[b] = mm->body_parentid[b];
     d->body_dofadr[b] = mm->body_dofadr[b];
     d->body_dofnum[b] = mm->body_dofnum[b];
+  }
+  for (int i = 0; i < mm->nsensor; i++) {  // the pipeline record's sensor lane records (fill_lane_records)
+    int depth = 0;
+    for (int bb = mm->site_bodyid[mm->sensor_objid[i]]; bb > 0; bb = mm->body_parentid[bb]) depth++;
+    if (depth > LS_MAXCH) return set_err(PP3_ERR_MODEL, "sensor site body deeper than 4 levels");
   }
   for (int a = 0; a < NU; a++) {
     int j = mm->actuator_trnid[a];

@@ -2,7 +2,7 @@
 # Round-5 GPU session (via gpurun): GPU suite, smoke, the driver's bench command (ls_cap,
 # idle_start), the A/B of ab/*.so, the host-API loop under a kernel + HIP trace, then the profile
 # recipe of the working-tree kernel.  Each GPU step has its own limit; a crash / timeout ends it.
-#   tools/gpu_r05.sh TAG [steps...]   steps: tests smoke driver ab hostapi prof policy
+#   tools/gpu_r05.sh TAG [steps...]   steps: tests smoke driver ab abdrv hostapi parts prof phases policy
 TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
@@ -45,6 +45,9 @@ for step in "$@"; do
       PP3_DIAG_OUT=$OUT DIAG_FUSED=1 timeout -k 10 300 python tests/diag_phases.py > $OUT/phases_fused.txt 2>&1 || { tail $OUT/phases_fused.txt; exit 1; }
       head -22 $OUT/phases_fused.txt
       python tools/trace_intervals.py $OUT/waves.npy 10,12,11,17,18,0 > $OUT/phases_fused_intervals.txt 2>&1; head -40 $OUT/phases_fused_intervals.txt ;;
+    parts)
+      timeout -k 10 300 python tools/host_api_parts.py 100 > $OUT/host_api_parts.txt 2>&1 || { tail $OUT/host_api_parts.txt; exit 1; }
+      cat $OUT/host_api_parts.txt ;;
     policy)
       timeout -k 10 300 python bench.py --policy 256,128,128 > $OUT/bench_policy.json 2> $OUT/bench_policy.err || { tail $OUT/bench_policy.err; exit 1; }
       python tools/bench_summary.py $OUT/bench_policy.json
