@@ -24,7 +24,8 @@ namespace pp3 {
 // lane k of a per-wave register accumulates phase k's cycles, one global atomic per lane at the
 // end of the launch (gfx950 has no SHADER_CYCLES hwreg).
 #ifdef PP3_PHASE_PROF
-constexpr int NPROF = 22;  // 0..18 phase cycles, 19 line-search evaluations per wave (max of its two envs), 20 per env
+constexpr int NPROF = 25;  // 0..18 phase cycles, 19 line-search evaluations per wave (max of its two envs), 20 per env,
+                           // 21..23 sub-phase cycles (line-search setup, Newton row update, warm-start row costs)
 struct Prof {
   uint32_t t, acc;
   uint32_t t0, dense, ncmax, evals;  // per wave: start stamp, dense-Hessian substeps, max contacts, line-search evaluations

@@ -54,10 +54,6 @@ constexpr float LS_NOISE = 64.0f;  // line-search convergence floor, in roundoff
 #ifndef PP3_COM_BF
 #define PP3_COM_BF 1
 #endif
-// PP3_CRB_BF (A/B): CRB x cdof and the RNE velocity chain as one straight-line block (crb_rne)
-#ifndef PP3_CRB_BF
-#define PP3_CRB_BF 0
-#endif
 // PP3_PIPE_V2: the pipeline record from flattened sensor records and one LDS round (write_pipeline)
 #ifndef PP3_PIPE_V2
 #define PP3_PIPE_V2 1
@@ -982,93 +978,6 @@ __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m,
   mul_inert_vec(s.x.a.F[l], crb, cdv);
 }
 
-#if PP3_CRB_BF
-// crb_times_cdof and rne_chain as one straight-line block (A/B): both phases' LDS operands in one
-// pinned round (clamped indices on the lanes that own nothing), their arithmetic interleaved by the
-// scheduler, the stores in lane branches at the end.  Same operations on the same operands.
-template <int NC>
-__device__ __forceinline__ void crb_rne(Shared<NC>& s, const DevModel& m, int l) {
-  // crb x cdof (lanes < NV)
-  const int lc = l < NV ? l : NV - 1;
-  const bool base = lc < 6;
-  const int b = base ? 2 : lc - 4, last = 2 + 3 * ((b - 2) / 3) + 2;
-  const float* r0 = base ? s.crb_base : s.cinert[b];
-  const int b1 = b + 1 <= last ? b + 1 : b, b2 = b + 2 <= last ? b + 2 : b;
-  float crb[10], c1[10], c2[10], cdv[6];
-#pragma unroll
-  for (int k = 0; k < 10; k++) { crb[k] = r0[k]; c1[k] = s.cinert[b1][k]; c2[k] = s.cinert[b2][k]; }
-#pragma unroll
-  for (int k = 0; k < 6; k++) cdv[k] = s.cdof[lc][k];
-  // rne chain (lanes 0..3: leg l & 3)
-  const int lg = l & 3;
-  float lcd[3][6], lqd[3], bcd[3][6], bq[6];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const int d = 6 + 3 * lg + k;
-#pragma unroll
-    for (int c = 0; c < 6; c++) lcd[k][c] = s.cdof[d][c];
-    lqd[k] = s.qvel[d];
-  }
-#pragma unroll
-  for (int d = 0; d < 3; d++)
-#pragma unroll
-    for (int k = 0; k < 6; k++) bcd[d][k] = s.cdof[3 + d][k];
-#pragma unroll
-  for (int k = 0; k < 6; k++) bq[k] = s.qvel[k];
-  PIN("+v"(crb[0]), "+v"(crb[1]), "+v"(crb[2]), "+v"(crb[3]), "+v"(crb[4]), "+v"(crb[5]), "+v"(crb[6]), "+v"(crb[7]),
-      "+v"(crb[8]), "+v"(crb[9]), "+v"(cdv[0]), "+v"(cdv[1]), "+v"(cdv[2]), "+v"(cdv[3]), "+v"(cdv[4]), "+v"(cdv[5]));
-  PIN("+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]), "+v"(c1[4]), "+v"(c1[5]), "+v"(c1[6]), "+v"(c1[7]),
-      "+v"(c1[8]), "+v"(c1[9]), "+v"(c2[0]), "+v"(c2[1]), "+v"(c2[2]), "+v"(c2[3]), "+v"(c2[4]), "+v"(c2[5]),
-      "+v"(c2[6]), "+v"(c2[7]), "+v"(c2[8]), "+v"(c2[9]));
-  PIN("+v"(lcd[0][0]), "+v"(lcd[0][1]), "+v"(lcd[0][2]), "+v"(lcd[0][3]), "+v"(lcd[0][4]), "+v"(lcd[0][5]),
-      "+v"(lcd[1][0]), "+v"(lcd[1][1]), "+v"(lcd[1][2]), "+v"(lcd[1][3]), "+v"(lcd[1][4]), "+v"(lcd[1][5]),
-      "+v"(lcd[2][0]), "+v"(lcd[2][1]), "+v"(lcd[2][2]), "+v"(lcd[2][3]), "+v"(lcd[2][4]), "+v"(lcd[2][5]),
-      "+v"(lqd[0]), "+v"(lqd[1]), "+v"(lqd[2]));
-  PIN("+v"(bcd[0][0]), "+v"(bcd[0][1]), "+v"(bcd[0][2]), "+v"(bcd[0][3]), "+v"(bcd[0][4]), "+v"(bcd[0][5]),
-      "+v"(bcd[1][0]), "+v"(bcd[1][1]), "+v"(bcd[1][2]), "+v"(bcd[1][3]), "+v"(bcd[1][4]), "+v"(bcd[1][5]),
-      "+v"(bcd[2][0]), "+v"(bcd[2][1]), "+v"(bcd[2][2]), "+v"(bcd[2][3]), "+v"(bcd[2][4]), "+v"(bcd[2][5]),
-      "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(bq[4]), "+v"(bq[5]));
-  const float w1 = (!base && b + 1 <= last) ? 1.0f : 0.0f, w2 = (!base && b + 2 <= last) ? 1.0f : 0.0f;
-#pragma unroll
-  for (int k = 0; k < 10; k++) crb[k] += w1 * c1[k];
-#pragma unroll
-  for (int k = 0; k < 10; k++) crb[k] += w2 * c2[k];
-  float F[6];
-  mul_inert_vec(F, crb, cdv);
-  float w[3] = {0, 0, 0}, bsum[3] = {0, 0, 0};
-#pragma unroll
-  for (int d = 0; d < 3; d++) {
-    const float q = bq[3 + d];
-#pragma unroll
-    for (int k = 0; k < 3; k++) { w[k] += bcd[d][k] * q; bsum[k] += bcd[d][3 + k] * q; }
-  }
-  const float v0 = bq[0], v1 = bq[1], v2 = bq[2];
-  float cv[6] = {w[0], w[1], w[2], v0 + bsum[0], v1 + bsum[1], v2 + bsum[2]};
-  float ca[6] = {0, 0, 0, -m.gravity[0] + (v1 * w[2] - v2 * w[1]), -m.gravity[1] + (v2 * w[0] - v0 * w[2]),
-                 -m.gravity[2] + (v0 * w[1] - v1 * w[0])};
-  float cvs[3][6], cas[3][6];
-  const float cv1[6] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5]}, ca1[6] = {ca[0], ca[1], ca[2], ca[3], ca[4], ca[5]};
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    float cdd[6];
-    cross_motion(cdd, cv, lcd[k]);
-    const float qd = lqd[k];
-    for (int c = 0; c < 6; c++) { cv[c] += lcd[k][c] * qd; ca[c] += cdd[c] * qd; }
-    for (int c = 0; c < 6; c++) { cvs[k][c] = cv[c]; cas[k][c] = ca[c]; }
-  }
-  if (l < NV)
-#pragma unroll
-    for (int k = 0; k < 6; k++) s.x.a.F[l][k] = F[k];
-  if (l == 0)
-    for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv1[k]; s.x.a.cacc[1][k] = ca1[k]; }
-  if (l < 4)
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int bb = 2 + 3 * l + k;
-      for (int c = 0; c < 6; c++) { s.cvel[bb][c] = cvs[k][c]; s.x.a.cacc[bb][c] = cas[k][c]; }
-    }
-}
-#endif
 
 // ------------------------------------------------------------------------------------
 // LDL^T in registers: lane i (< NV) of each half holds row i; returns L_ik (k<i) in a[k],
@@ -1679,11 +1588,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
-#if PP3_CRB_BF
-  { crb_rne(s, m, l); SYNC(); }
-#else
   { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
-#endif
   PHASE(15); l = opaque_lane(l);
   int lsup = 4;  // lane c: support of contact c (4 = none)
   { lsup = collision<NC, NWV>(s, m, l, h, pair_pf); SYNC(); }
@@ -1944,6 +1849,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       cws += isfr[t] ? f1 : ((x1 < 0) ? q1 : 0.0f);
       csm += isfr[t] ? f2 : ((x2 < 0) ? q2 : 0.0f);
     }
+    PHASE(23);  // (prof build: warm-start row costs; phase 5 is then M qws, the sums and the choice)
     if (l < NV) {  // lane l: dof dn = pnat(l), the row it holds in mrow
       const int dn = pnat(l);
       ma_ws = mrow_dot_reg(mrow, s.qws);
@@ -1988,6 +1894,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       s.efc_D[r] = Dq;  // active D (0 when not quadratic) for the Hessian
     }
     SYNC();
+    PHASE(22);  // (prof build: constraint state update; phase 6 is then the gradient and G blocks)
     // gradient, diagonal D per dof, contact Hessian blocks
     float gauss = 0;
     if (l < NV) {  // lane l: dof dn = pnat(l) (its (M qacc) entry is ma)
@@ -2165,6 +2072,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     sn = sqrtf(hsum(sn, h));
     live = live && !(sn < MINVAL);
     const float gtol = m.gtol_scale * sn;
+    PHASE(21);  // (prof build: the line search's setup ends here; phase 8 is then its evaluations)
     auto eval = [&](float alpha, float& cost, float& d0, float& d1) {
       float t0, t1, t2;
       pieces(alpha, t0, t1, t2);

@@ -24,6 +24,8 @@ NAMES = ["kinematics", "com/cinert/cdof", "limit/friction rows+actuation", "M+bi
          "warmstart", "newton update+grad", "LDL(H)+solve", "line search", "integrate",
          "prologue", "write_obs (history)", "rewards+state", "bias+contact edge rows", "hessian build",
          "crb*cdof+rne chain", "collision", "obs rng draws", "imu + lag buffers"]
+# stamps 21..23 split phases 8 (line search), 6 (newton update+grad) and 5 (warmstart)
+SUBNAMES = ["  line-search setup", "  newton row update", "  warmstart row costs"]
 
 
 def main():
@@ -40,18 +42,21 @@ def main():
     _lib.check(L.pp3_fill_uniform(env._h, acts.ptr, (steps + warm) * E * 12, 1, 0, -1.0, 1.0, None))
     ms = C.c_float()
     _lib.check(L.pp3_step_timed(env._h, acts.ptr, E * 12, warm, C.byref(ms)))
-    buf = (C.c_uint64 * 22)()
-    _lib.check(L.pp3_phase_profile(buf, 22, 1))
+    buf = (C.c_uint64 * 25)()
+    _lib.check(L.pp3_phase_profile(buf, 25, 1))
     if os.environ.get("DIAG_FUSED") == "1":  # one pp3_rollout launch (trace: its second step)
         _lib.check(L.pp3_rollout_timed(env._h, C.c_void_p(acts.ptr.value + warm * E * 48), E * 12, steps,
                                        None, None, None, C.byref(ms)))
     else:
         _lib.check(L.pp3_step_timed(env._h, C.c_void_p(acts.ptr.value + warm * E * 48), E * 12, steps, C.byref(ms)))
-    _lib.check(L.pp3_phase_profile(buf, 22, 1))
+    _lib.check(L.pp3_phase_profile(buf, 25, 1))
     v = np.array(buf[:len(NAMES)], dtype=np.float64)
-    tot = v.sum()
+    sub = np.array(buf[21:24], dtype=np.float64)  # sub-phases split off phases 8, 6, 5
+    tot = v.sum() + sub.sum()
     print(f"E={E}: {ms.value / steps:.3f} ms/step (prof build); cycles per env-step per env: {tot / (E * steps):.0f}")
     for n, x in zip(NAMES, v):
+        print(f"  {n:32s} {100 * x / tot:6.2f}%   {x / (E * steps):10.0f} cyc/env-step")
+    for n, x in zip(SUBNAMES, sub):
         print(f"  {n:32s} {100 * x / tot:6.2f}%   {x / (E * steps):10.0f} cyc/env-step")
     # per-wave record of the last launch: the kernel ends with its slowest wave
     W = (E + 1) // 2
