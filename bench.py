@@ -841,6 +841,8 @@ def main():
             "gpu_prewarm_ms": round(prewarm_ms, 1),
             "ms_per_step": round(wall_max / K * 1e3, 4),
             "state_sha16": state_sha16,
+            # the step kernel's sources (profiles/README.md names each version by this hash)
+            "kernel_src_sha16": kernel_source_sha16(),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
