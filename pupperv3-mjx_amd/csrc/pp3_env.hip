@@ -54,15 +54,6 @@ constexpr float LS_NOISE = 64.0f;  // line-search convergence floor, in roundoff
 #ifndef PP3_COM_BF
 #define PP3_COM_BF 1
 #endif
-// PP3_PAIR_PF_AT (A/B): where the substep issues the narrow phase's first pair-record loads
-// (0 substep start, 1 after kinematics, 2 after com)
-#ifndef PP3_PAIR_PF_AT
-#define PP3_PAIR_PF_AT 2
-#endif
-// PP3_RM_PF_AT (A/B): where the M-entry phase's lane records are loaded (0 substep start, 2 after com)
-#ifndef PP3_RM_PF_AT
-#define PP3_RM_PF_AT 0
-#endif
 // PP3_PIPE_V2: the pipeline record from flattened sensor records and one LDS round (write_pipeline)
 #ifndef PP3_PIPE_V2
 #define PP3_PIPE_V2 1
@@ -1584,38 +1575,20 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
 #pragma unroll
     for (int k = 0; k < 2; k++)
       for (int c = 0; c < 4; c++) rc_pf.f[4 * k + c] = v[k][c];
-#if PP3_RM_PF_AT == 0
 #pragma unroll
     for (int k = 0; k < 3; k++) v[2 + k] = *reinterpret_cast<const v4f*>(m.lane_m.g[k][l]);
 #pragma unroll
     for (int k = 0; k < 3; k++)
       for (int c = 0; c < 4; c++) rm_pf.f[4 * k + c] = v[2 + k][c];
-#endif
   }
-  // the narrow phase's pair records for this lane's first pair, likewise (model constants)
-#if PP3_PAIR_PF_AT == 0
-  const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
-#endif
   kinematics(s, m, l, integrate_prev, kc); SYNC();
   PHASE(0); l = opaque_lane(l);
-#if PP3_PAIR_PF_AT == 1
-  const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
-#endif
   { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
-#if PP3_PAIR_PF_AT == 2
+  // the narrow phase's pair records for this lane's first pair, loaded without a wait: they arrive
+  // during CRB x cdof and the RNE chain (issued at the substep start they measured 0.3 % slower in
+  // v22: 28 more registers live through kinematics and com)
   const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
-#endif
-#if PP3_RM_PF_AT == 2
-  {
-    v4f v[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) v[k] = *reinterpret_cast<const v4f*>(m.lane_m.g[k][l]);
-#pragma unroll
-    for (int k = 0; k < 3; k++)
-      for (int c = 0; c < 4; c++) rm_pf.f[4 * k + c] = v[k][c];
-  }
-#endif
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
   { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
