@@ -118,9 +118,11 @@ def _ro(a):
 
 class DeviceState(State):
     """A State returned by PupperV3Env.reset / step (the host surface of the
-    device-resident env).  step() returns before its launch has finished: obs / reward / done are
-    views of the page-locked block the launch stores into, made (after waiting for that launch's
-    completion event) on first access.  pipeline_state, metrics, info (and the raw record) are
+    device-resident env).  step() returns before its launch has finished -- with DEFER_LAUNCH before
+    it is even issued: the env issues it at its next device operation or when this state's fields
+    are first read (PupperV3Env._flush).  obs / reward / done are views of the page-locked block
+    the launch stores into, made (after waiting for that launch's completion event) on first
+    access.  pipeline_state, metrics, info (and the raw record) are
     downloaded on first access -- from the env's live buffers while the env has not launched since,
     else from a device snapshot the env took just before its next launch
     (PupperV3Env._before_launch), so an old state always reads its own data.  Every array is
