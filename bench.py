@@ -286,14 +286,30 @@ def host_api_rates(model_path, E, device, keys, steps=30, warmup=3):
                     else:
                         for i in range(steps):
                             st = api.step(st, acts[a0 + i])
+                        _ = st.obs[0, 0]  # the window ends when the last step's outputs are on the host
                     best = max(best, E * steps / (time.perf_counter() - t))
                 name = ("wrap(env)" if wrapped else "env") + (f".rollout(K={steps})" if roll else ".step")
                 out[name + ("" if pipe else " [pipeline_output=False]")] = round(best, 1)
+                if not roll and not wrapped and pipe:
+                    # a host policy's loop: the caller reads every step's observation before the next
+                    best = 0.0
+                    for w in range(2):
+                        a0 = warmup + w * steps
+                        t = time.perf_counter()
+                        for i in range(steps):
+                            st = api.step(st, acts[a0 + i])
+                            _ = st.obs[0, 0]
+                        best = max(best, E * steps / (time.perf_counter() - t))
+                    out["env.step, obs read every step"] = round(best, 1)
                 env.close()
     out["per_step_pcie_bytes"] = {"h2d_actions": E * 12 * 4, "d2h_obs_reward_done": E * (72 + 2) * 4}
-    out["note"] = ("env-steps/s through the host API (numpy in, numpy out; step: one host sync per step, "
-                   "rollout: one per K steps, the K-step trajectory stored by the launch into page-locked host "
-                   "memory); the device path is `value`")
+    out["note"] = ("env-steps/s through the host API (numpy in, numpy out; step: asynchronous, the launches "
+                   "issued when a queued state is read or the queue holds environment.STEP_BATCH steps, "
+                   "consecutive steps fused into one launch, obs / reward / done stored by it into "
+                   "page-locked host memory, the window closed by reading the last step's obs; "
+                   "'obs read every step': the loop reads each step's observation before the next step, as "
+                   "a host policy does; rollout: one launch and one sync per K steps, the K-step trajectory "
+                   "stored into page-locked host memory); the device path is `value`")
     return out
 
 

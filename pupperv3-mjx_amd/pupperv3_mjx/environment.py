@@ -102,11 +102,16 @@ ASYNC_DEPTH = 2
 # step(): the launch reads the actions straight from the page-locked staging block through its device
 # mapping instead of after a copy-engine transfer into a device buffer
 ACTIONS_ZERO_COPY = True
-# step() (with ASYNC_STEP) queues its launch and issues it at the env's next device operation (the
-# next step, any other call into the library, or the first read of the returned state's fields): by
-# then the caller of `state = env.step(state, action)` has dropped the state the launch overwrites,
-# so no device snapshot of it is taken (PupperV3Env._flush)
+# step() (with ASYNC_STEP) queues its launch and issues it at the env's next device operation (a
+# step from another state, any other call into the library, or the first read of a queued state's
+# fields): by then the caller of `state = env.step(state, action)` has dropped the states the launch
+# overwrites, so no device snapshot of them is taken (PupperV3Env._flush)
 DEFER_LAUNCH = True
+# steps queued from one another (each from the state the previous returned) run as ONE fused
+# pp3_rollout launch of up to STEP_BATCH steps when they are issued -- bit-equal to single-step
+# launches; a queued state still alive at issue ends a launch of its own, so its lazy fields
+# (info, metrics, pipeline_state) exist on the device; 1 = one launch per step
+STEP_BATCH = 16
 
 
 def _ro(a):
@@ -173,10 +178,15 @@ class DeviceState(State):
         ready = self.__dict__.get("_ready")
         if ready is None:
             return
-        lease, slot = ready
         self._env._flush_for(self)
-        slot.wait()
-        obs, rew, done = self._env._output_views(lease, self._single)
+        if isinstance(ready[0], _StepBatch):  # step j of a batch (STEP_BATCH)
+            batch, j = ready
+            batch.slot.wait()
+            obs, rew, done = batch.views(j, self._single)
+        else:
+            lease, slot = ready
+            slot.wait()
+            obs, rew, done = self._env._output_views(lease, self._single)
         self.__dict__.update(obs=obs, reward=rew, done=done, _out=(obs, rew, done), _ready=None)
 
     def _materialize(self) -> None:
@@ -401,8 +411,8 @@ class PupperV3Env:
         _lib.check(L.pp3_create(C.byref(m), C.byref(c), self.num_envs, self.device, C.byref(h)))
         self._h = h
         self._raw = L
-        self._pending = None
-        self._L = _FlushingLib(self, L)  # every call into the library issues a queued step first
+        self._qb = None
+        self._L = _FlushingLib(self, L)  # every call into the library issues the queued steps first
         assert int(L.pp3_state_stride(h)) == self.stride
         _lib.check(L.pp3_set_pipeline_output(h, int(pipeline_output)))
         self._keys_buf = _lib.DeviceBuffer(self.num_envs * 8, self.device)
@@ -415,14 +425,16 @@ class PupperV3Env:
         buffers, the last issued state, and a pool of device snapshots of its lazy fields."""
         self._gen = 0
         self._issued = None
-        self._pending = None  # a step() launch queued for the next device operation (DEFER_LAUNCH)
+        self._qb = None  # the steps queued for the next device operation (_StepBatch; DEFER_LAUNCH)
+        self._batch_pool = _lib.BlockPool()  # page-locked output blocks of step batches
         self._n_snapshots = 0  # device snapshots taken of issued states (_before_launch)
         self._snap_pool = []
         self._pin_pool = _lib.BlockPool()  # page-locked output blocks (obs | reward | done) of issued states
         self._traj_pool = {}   # page-locked rollout trajectory blocks, per unroll length
         # page-locked action staging: a ring of ASYNC_DEPTH blocks, each reused only after the launch
         # that read it has completed (its event)
-        self._act_ring = [_ActSlot(self, self.num_envs * _abi.NU * 4) for _ in range(max(1, ASYNC_DEPTH))]
+        self._act_ring = [_ActSlot(self, max(1, STEP_BATCH) * self.num_envs * _abi.NU * 4)
+                          for _ in range(max(1, ASYNC_DEPTH))]
         self._act_i = 0
         self._lazy_extra = {}  # field id -> info hook (wrappers.AutoResetEpisodeEnv: the episode record)
         self._issue_capture = None  # () -> host data a wrapper attaches to each state when it is issued
@@ -527,6 +539,8 @@ class PupperV3Env:
         # free page-locked blocks go with their pools; leased ones are freed when their arrays die
         if getattr(self, "_pin_pool", None) is not None:
             self._pin_pool.retire()
+        if getattr(self, "_batch_pool", None) is not None:
+            self._batch_pool.retire()
         for pool in (getattr(self, "_traj_pool", None) or {}).values():
             pool.retire()
         for slot in getattr(self, "_act_ring", None) or ():
@@ -617,6 +631,8 @@ class PupperV3Env:
         return self._issue(single)
 
     def step(self, state: State, action) -> State:
+        if ASYNC_STEP and DEFER_LAUNCH and STEP_WRITES_HOST:
+            return self._step_queued(state, action)
         self._flush()
         single = _single_of(state)
         act = np.ascontiguousarray(np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU))
@@ -627,7 +643,7 @@ class PupperV3Env:
         slot = self._act_ring[self._act_i]
         self._act_i = (self._act_i + 1) % len(self._act_ring)
         slot.wait()
-        np.copyto(slot.arr, act.reshape(-1))
+        np.copyto(slot.arr[:act.size], act.reshape(-1))
         if ACTIONS_ZERO_COPY:
             act_ptr = C.c_void_p(slot.block.device_ptr())
         else:  # copied on the env's stream ahead of the launch
@@ -643,12 +659,6 @@ class PupperV3Env:
         n, D = self.num_envs, self.observation_size
         lease = _lib.PinnedBlock.take(4 * n * (D + 2), self._pin_pool)
         dev = lease.device_ptr()
-        if ASYNC_STEP and DEFER_LAUNCH:
-            # the state this launch will leave on the device (its generation is the env's after it)
-            st = DeviceState(self, self._gen + 1, single, ready=(lease, slot))
-            st.__dict__["_capture"] = self._issue_capture() if self._issue_capture is not None else None
-            self._pending = (act_ptr.value, dev, slot, weakref.ref(st))
-            return st
         self._before_launch()
         _lib.check(self._L.pp3_rollout(self._h, act_ptr, 0, 1, C.c_void_p(dev + 4 * n * D),
                                        C.c_void_p(dev + 4 * n * (D + 1)), C.c_void_p(dev), None))
@@ -668,27 +678,68 @@ class PupperV3Env:
         _lib.check(self._L.pp3_rollout(self._h, C.c_void_p(actions_dev), int(action_stride), int(nsteps),
                                        vp(reward_dev), vp(done_dev), vp(obs_dev), vp(stream)))
 
+    def _step_queued(self, state: State, action) -> State:
+        """step() with DEFER_LAUNCH: the step joins the queued batch when `state` is the batch's last
+        state (the loop `state = env.step(state, action)`), else the queue is issued first and a new
+        batch starts from `state`.  Nothing is launched here (see _flush)."""
+        single = _single_of(state)
+        act = np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU)
+        qb = self._qb
+        if qb is not None and (qb.n >= max(1, STEP_BATCH) or qb.tail() is not state):
+            self._flush()
+            qb = None
+        if qb is None:
+            if not self.holds(state):
+                self._write_state(state)
+            # a page-locked action block of the ring (reused once the launch that read it completed)
+            slot = self._act_ring[self._act_i]
+            self._act_i = (self._act_i + 1) % len(self._act_ring)
+            slot.wait()
+            n, D, B = self.num_envs, self.observation_size, max(1, STEP_BATCH)
+            lease = _lib.PinnedBlock.take(4 * B * n * (D + 2), self._batch_pool)
+            qb = self._qb = _StepBatch(self, slot, lease, B)
+        j = qb.n
+        np.copyto(qb.act[j], act)
+        st = DeviceState(self, qb.gen0 + j + 1, single, ready=(qb, j))
+        st.__dict__["_capture"] = self._issue_capture() if self._issue_capture is not None else None
+        qb.states.append(weakref.ref(st))
+        qb.n += 1
+        return st
+
     def _flush_for(self, st: "DeviceState") -> None:
-        """Issue the queued launch if `st` is the state it returns (its outputs are wanted)."""
-        p = self._pending
-        if p is not None and p[3]() is st:
+        """Issue the queued steps if `st` is one of them (its outputs are wanted)."""
+        qb = self._qb
+        if qb is not None and any(r() is st for r in qb.states):
             self._flush()
 
     def _flush(self) -> None:
-        """Issue the step() launch queued by DEFER_LAUNCH (no-op when none is): first the device
-        snapshot of the state it overwrites, if that state is still alive and unread
-        (_before_launch), then the launch and its completion event."""
-        p = self._pending
-        if p is None:
+        """Issue the steps queued by DEFER_LAUNCH (no-op when none are): fused pp3_rollout launches
+        that end at every queued state still alive and at the last one (a dropped state's device
+        fields are never needed; a live one's are snapshotted before the next launch overwrites
+        them, _before_launch), each storing its steps' obs | reward | done into the batch's
+        page-locked block; then the completion event of the batch's action block."""
+        qb = self._qb
+        if qb is None:
             return
-        self._pending = None
-        act, dev, slot, stref = p
-        self._before_launch()
-        n, D = self.num_envs, self.observation_size
-        _lib.check(self._raw.pp3_rollout(self._h, C.c_void_p(act), 0, 1, C.c_void_p(dev + 4 * n * D),
-                                         C.c_void_p(dev + 4 * n * (D + 1)), C.c_void_p(dev), None))
-        slot.record()
-        self._issued = stref
+        self._qb = None
+        if qb.n == 0:
+            return
+        n, D, B = self.num_envs, self.observation_size, qb.cap
+        dev = qb.lease.device_ptr()
+        act_dev = qb.slot.block.device_ptr()
+        ends = [j for j, r in enumerate(qb.states) if j == qb.n - 1 or r() is not None]
+        start = 0
+        for e in ends:
+            K = e - start + 1
+            self._before_launch()
+            _lib.check(self._raw.pp3_rollout(
+                self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU, K,
+                C.c_void_p(dev + 4 * (B * n * D + start * n)), C.c_void_p(dev + 4 * (B * n * (D + 1) + start * n)),
+                C.c_void_p(dev + 4 * start * n * D), None))
+            self._gen = qb.gen0 + e + 1
+            self._issued = qb.states[e]
+            start = e + 1
+        qb.slot.record()
 
     def rollout(self, state: State, actions) -> Tuple[State, Dict[str, np.ndarray]]:
         """The unroll of brax's generate_unroll ([ext] brax 0.12.1 training/acting.py: a lax.scan of
@@ -801,6 +852,9 @@ class PupperV3Env:
     def holds(self, state: State) -> bool:
         """The device buffers hold exactly `state`: the last state this env issued, unedited, and
         no launch or upload since."""
+        qb = self._qb
+        if qb is not None and qb.n and qb.tail() is state:
+            return True  # the queued steps' last state (held once they are issued; never edited before)
         self._flush()  # (a queued step's state is held once its launch is issued)
         return (isinstance(state, DeviceState) and state.__dict__.get("_env") is self and state._gen == self._gen
                 and state.unedited())
@@ -973,6 +1027,35 @@ def _single_of(state) -> bool:
     return np.ndim(state.reward) == 0
 
 
+class _StepBatch:
+    """Steps queued by PupperV3Env.step (DEFER_LAUNCH): their actions in one page-locked block of the
+    env's ring ([cap][N][12]) and their outputs in one page-locked block ([cap][N][36H] obs |
+    [cap][N] reward | [cap][N] done), each queued state viewing its own rows."""
+
+    def __init__(self, env: "PupperV3Env", slot, lease, cap: int):
+        n = env.num_envs
+        self.slot, self.lease, self.cap = slot, lease, cap
+        self.act = slot.arr[:cap * n * _abi.NU].reshape(cap, n, _abi.NU)
+        self.n_envs, self.D = n, env.observation_size
+        self.gen0 = env._gen
+        self.states = []  # weak references to the queued states, in order
+        self.n = 0
+
+    def tail(self):
+        return self.states[-1]() if self.states else None
+
+    def views(self, j: int, single: bool):
+        """(obs, reward, done) read-only views of step j's rows; they keep the block leased."""
+        n, D, B = self.n_envs, self.D, self.cap
+        flat = np.asarray(self.lease)
+        obs = _ro(flat[j * n * D:(j + 1) * n * D].reshape(n, D))
+        rew = _ro(flat[B * n * D + j * n:B * n * D + (j + 1) * n])
+        done = _ro(flat[B * n * (D + 1) + j * n:B * n * (D + 1) + (j + 1) * n])
+        if single:
+            obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
+        return obs, rew, done
+
+
 class _FlushingLib:
     """The library as PupperV3Env._L: each call first issues the env's queued step() launch
     (DEFER_LAUNCH), so whatever reads or changes the device sees the state step() returned."""
@@ -987,7 +1070,7 @@ class _FlushingLib:
 
         def call(*args):
             env = env_ref()
-            if env is not None and env.__dict__.get("_pending") is not None:
+            if env is not None and env.__dict__.get("_qb") is not None:
                 env._flush()
             return fn(*args)
         call.__name__ = name

@@ -271,10 +271,11 @@ def test_async_steps_match_synchronous_steps(require_gpu, zero_copy):
 
 
 def test_deferred_step_loop_takes_no_snapshots(require_gpu):
-    """`state = env.step(state, action)` with DEFER_LAUNCH: each launch is issued at the next call,
-    after the caller has dropped the state it overwrites, so the loop takes no device snapshot and
-    ends bit for bit where the synchronous loop does; a state the caller keeps is still snapshotted
-    and reads its own record; reading a returned state's fields issues its launch."""
+    """`state = env.step(state, action)` with DEFER_LAUNCH: the steps queue and run as fused launches
+    once a queued state's fields are read, after the caller has dropped the states they overwrite,
+    so the loop takes no device snapshot and ends bit for bit where the synchronous loop does; a
+    state the caller keeps ends a launch of its own, is snapshotted before the next one and reads
+    its own record."""
     from pupperv3_mjx import environment
     saved = environment.ASYNC_STEP, environment.DEFER_LAUNCH
     acts = np.random.RandomState(12).uniform(-1, 1, size=(9, N, 12)).astype(np.float32)
@@ -293,18 +294,70 @@ def test_deferred_step_loop_takes_no_snapshots(require_gpu):
         st = e.reset(make_keys(13, N))
         for t in range(6):
             st = e.step(st, acts[t])
-        assert e._n_snapshots == 0 and e._pending is not None
-        kept = st  # kept past the next two steps: snapshotted when the launch after it is issued
+        assert e._n_snapshots == 0 and e._qb is not None and e._qb.n == 6  # queued, nothing launched
+        kept = st
         for t in range(6, 9):
             st = e.step(st, acts[t])
-        assert e._n_snapshots == 1
-        np.testing.assert_array_equal(kept._record, recs[5])
-        np.testing.assert_array_equal(st.obs, ref_obs)  # (issues the last queued launch)
-        assert e._pending is None
+        assert e._n_snapshots == 0 and e._qb.n == 9
+        np.testing.assert_array_equal(kept._record, recs[5])  # (issues the queue: launches end at 5 and 8)
+        assert e._qb is None and e._n_snapshots == 1
+        np.testing.assert_array_equal(st.obs, ref_obs)
         np.testing.assert_array_equal(st._record, recs[8])
         e.close()
     finally:
         environment.ASYNC_STEP, environment.DEFER_LAUNCH = saved
+
+
+@pytest.mark.parametrize("keep", ["states", "batches"])
+@pytest.mark.parametrize("wrapped", [False, True])
+def test_step_batches_match_synchronous_steps(require_gpu, keep, wrapped):
+    """Queued steps issued as fused launches (STEP_BATCH = 4: 11 steps are batches of 4, 4 and 3)
+    give every step's obs / reward / done, and every kept state's record, bit for bit as the
+    synchronous loop: with every state kept (each ends a launch of its own: one-step launches) and
+    with the states dropped (four- and three-step launches; the rows read from the batches'
+    page-locked blocks), also through the wrapper (on-device auto-reset inside the fused launches)."""
+    from pupperv3_mjx import environment
+    saved = environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH
+    acts = np.random.RandomState(14).uniform(-1, 1, size=(11, N, 12)).astype(np.float32)
+    try:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH = False, False
+        e = _env()
+        api = wrappers.wrap(e, episode_length=5) if wrapped else e
+        st = api.reset(make_keys(15, N))
+        ref = []
+        for t in range(11):
+            st = api.step(st, acts[t])
+            ref.append((np.array(st.obs), np.array(st.reward), np.array(st.done), np.array(st._record)))
+        e.close()
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = True, True, 4
+        e = _env()
+        api = wrappers.wrap(e, episode_length=5) if wrapped else e
+        st = api.reset(make_keys(15, N))
+        kept, batches = [], []
+        for t in range(11):
+            st = api.step(st, acts[t])
+            if keep == "states":
+                kept.append(st)
+            elif e._qb is not None and (not batches or batches[-1] is not e._qb):
+                batches.append(e._qb)
+        np.testing.assert_array_equal(st._record, ref[-1][3])  # (issues the last batch)
+        e.synchronize()
+        if keep == "states":
+            for k, (o, r, d, rec) in zip(kept, ref):
+                np.testing.assert_array_equal(k.obs, o)
+                np.testing.assert_array_equal(k.reward, r)
+                np.testing.assert_array_equal(k.done, d)
+                np.testing.assert_array_equal(k._record, rec)
+        else:
+            assert [b.n for b in batches] == [4, 4, 3] and e._n_snapshots == 0
+            rows = [b.views(j, False) for b in batches for j in range(b.n)]
+            for (go, gr, gd), (o, r, d, _) in zip(rows, ref):
+                np.testing.assert_array_equal(go, o)
+                np.testing.assert_array_equal(gr, r)
+                np.testing.assert_array_equal(gd, d)
+        e.close()
+    finally:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = saved
 
 
 def test_retired_pools_free_their_blocks(require_gpu):

@@ -28,7 +28,7 @@ for step in "$@"; do
       REPS=${REPS:-4} STEPS=20 bash tools/ab_bench.sh > $OUT/ab_driver.txt 2>&1 || { tail $OUT/ab_driver.txt; exit 1; }
       cat $OUT/ab_driver.txt ;;
     hostapi)
-      for mode in sync async async_zc defer sync async async_zc defer; do
+      for mode in sync async_zc defer1 defer defer_read sync async_zc defer1 defer defer_read; do
         for pipe in 1 0; do
           timeout -k 10 200 python tools/host_api_trace.py 200 $pipe $mode >> $OUT/host_api_plain.txt 2>&1 || { tail $OUT/host_api_plain.txt; exit 1; }
         done
