@@ -360,6 +360,57 @@ def test_step_batches_match_synchronous_steps(require_gpu, keep, wrapped):
         environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = saved
 
 
+def test_step_queue_mixed_with_rollout_branch_and_reset(require_gpu):
+    """The step queue (DEFER_LAUNCH, STEP_BATCH) between other calls: a rollout() from the queued
+    tail, a step from an older kept state (a branch: the queue is issued, the old state re-uploaded
+    from its snapshot), a reset() while steps are queued, and reads in between -- every state's
+    obs / reward / done / record bit for bit the synchronous sequence's."""
+    from pupperv3_mjx import environment
+    saved = environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH
+    acts = np.random.RandomState(16).uniform(-1, 1, size=(16, N, 12)).astype(np.float32)
+
+    def run(e):
+        out = {}
+        st = e.reset(make_keys(17, N))
+        st = e.step(st, acts[0])
+        s1 = st                                  # kept, read only at the end
+        st = e.step(st, acts[1])
+        st = e.step(st, acts[2])
+        st, tr = e.rollout(st, acts[3:6])        # from the queued tail
+        out["traj"] = tr
+        st = e.step(st, acts[6])
+        st = e.step(st, acts[7])
+        out["mid_obs"] = np.array(st.obs)        # read between queued steps
+        st = e.step(st, acts[8])
+        b = e.step(s1, acts[9])                  # branch from an old state
+        b = e.step(b, acts[10])
+        st = e.step(st, acts[11])                # and back to the main line
+        r = e.reset(make_keys(18, N))            # reset with steps queued
+        r = e.step(r, acts[12])
+        r = e.step(r, acts[13])
+        for name, x in (("s1", s1), ("main", st), ("branch", b), ("reset", r)):
+            out[name] = (np.array(x.obs), np.array(x.reward), np.array(x.done), np.array(x._record))
+        return out
+
+    try:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH = False, False
+        e = _env()
+        ref = run(e)
+        e.close()
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = True, True, 4
+        e = _env()
+        got = run(e)
+        e.close()
+        for k in ref["traj"]:
+            np.testing.assert_array_equal(got["traj"][k], ref["traj"][k])
+        np.testing.assert_array_equal(got["mid_obs"], ref["mid_obs"])
+        for name in ("s1", "main", "branch", "reset"):
+            for g, r in zip(got[name], ref[name]):
+                np.testing.assert_array_equal(g, r)
+    finally:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = saved
+
+
 def test_retired_pools_free_their_blocks(require_gpu):
     """A page-locked block leased from a pool the env has retired (a trajectory length no longer
     used, or a closed env) is freed when released, not parked in the orphaned pool (advisor r04)."""
