@@ -170,6 +170,8 @@ def rest_penetration(pair, mass, g_normal, radius, impratio, timestep):
         hi *= 2
     for _ in range(200):
         mid = 0.5 * (lo + hi)
+        if mid == lo or mid == hi:  # the bracket is one ulp wide: further halvings change nothing
+            break
         lo, hi = (mid, hi) if load(mid) < mass * g_normal else (lo, mid)
     return 0.5 * (lo + hi)
 
@@ -201,6 +203,8 @@ def steady_creep(pair, mass, radius, theta, g, impratio, timestep):
             hi += 2 * (hi - lo)
         for _ in range(200):
             mid = 0.5 * (lo + hi)
+            if mid == lo or mid == hi:  # (one ulp wide: the same result as the full 200 halvings)
+                break
             lo, hi = (mid, hi) if f(mid) > 0 else (lo, mid)
         return 0.5 * (lo + hi)
 
