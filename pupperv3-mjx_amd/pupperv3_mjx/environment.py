@@ -112,6 +112,11 @@ DEFER_LAUNCH = True
 # launches; a queued state still alive at issue ends a launch of its own, so its lazy fields
 # (info, metrics, pipeline_state) exist on the device; 1 = one launch per step
 STEP_BATCH = 16
+# a launch of queued steps stores obs / reward / done into page-locked host memory for its last step
+# only (the state that ends it): the states before it were dropped, so nothing can read their rows,
+# and each row is 1.2 MB of PCIe stores at 4096 envs.  The steps before are one launch without
+# trajectory outputs, the last a launch of its own (bit-equal: a fused launch equals single steps)
+LIVE_OUTPUTS_ONLY = True
 
 
 def _ro(a):
@@ -426,7 +431,8 @@ class PupperV3Env:
         self._gen = 0
         self._issued = None
         self._qb = None  # the steps queued for the next device operation (_StepBatch; DEFER_LAUNCH)
-        self._batch_pool = _lib.BlockPool()  # page-locked output blocks of step batches
+        self._batch_pool = _lib.BlockPool()
+        self._batch_spares = False  # the pool holds its spares (_step_queued)
         self._n_snapshots = 0  # device snapshots taken of issued states (_before_launch)
         self._snap_pool = []
         self._pin_pool = _lib.BlockPool()  # page-locked output blocks (obs | reward | done) of issued states
@@ -697,6 +703,13 @@ class PupperV3Env:
             slot.wait()
             n, D, B = self.num_envs, self.observation_size, max(1, STEP_BATCH)
             lease = _lib.PinnedBlock.take(4 * B * n * (D + 2), self._batch_pool)
+            if not self._batch_spares:
+                # a step loop cycles through ASYNC_DEPTH + 1 output blocks (the batch in flight, the
+                # one queuing, the one whose tail state is still the caller's): allocated now, not
+                # as a multi-millisecond page-locked allocation in the middle of the loop
+                self._batch_spares = True
+                for _ in range(max(1, ASYNC_DEPTH)):
+                    self._batch_pool.append(_lib.PinnedBlock(4 * B * n * (D + 2)))
             qb = self._qb = _StepBatch(self, slot, lease, B)
         j = qb.n
         np.copyto(qb.act[j], act)
@@ -716,8 +729,9 @@ class PupperV3Env:
         """Issue the steps queued by DEFER_LAUNCH (no-op when none are): fused pp3_rollout launches
         that end at every queued state still alive and at the last one (a dropped state's device
         fields are never needed; a live one's are snapshotted before the next launch overwrites
-        them, _before_launch), each storing its steps' obs | reward | done into the batch's
-        page-locked block; then the completion event of the batch's action block."""
+        them, _before_launch), each storing the obs | reward | done of the state that ends it (with
+        LIVE_OUTPUTS_ONLY; else of all its steps) into the batch's page-locked block; then the
+        completion event of the batch's action block."""
         qb = self._qb
         if qb is None:
             return
@@ -730,10 +744,13 @@ class PupperV3Env:
         ends = [j for j, r in enumerate(qb.states) if j == qb.n - 1 or r() is not None]
         start = 0
         for e in ends:
-            K = e - start + 1
             self._before_launch()
+            if LIVE_OUTPUTS_ONLY and e > start:  # steps start .. e-1: dropped states, no host rows
+                _lib.check(self._raw.pp3_rollout(self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU,
+                                                 e - start, None, None, None, None))
+                start = e
             _lib.check(self._raw.pp3_rollout(
-                self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU, K,
+                self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU, e - start + 1,
                 C.c_void_p(dev + 4 * (B * n * D + start * n)), C.c_void_p(dev + 4 * (B * n * (D + 1) + start * n)),
                 C.c_void_p(dev + 4 * start * n * D), None))
             self._gen = qb.gen0 + e + 1

@@ -2,7 +2,7 @@
 the host API's time per step goes).  4096 envs (bench.py workload), 20 untimed steps, then `N`
 timed env.step(state, numpy actions) calls; prints us/step.
 
-  python tools/host_api_trace.py [N] [pipeline_output 0|1] [sync|async|async_zc|defer1|defer|defer_read]
+  python tools/host_api_trace.py [N] [pipeline_output 0|1] [sync|async|async_zc|defer1|defer|defer_all|defer_read]
 
 Modes: sync = every step synchronises before it returns (the round-4 host API); async = step()
 returns at once, obs / reward / done wait for their own launch (environment.ASYNC_STEP); async_zc =
@@ -10,7 +10,9 @@ async, and the launch reads the actions straight from the page-locked staging bl
 (environment.ACTIONS_ZERO_COPY); defer = async_zc with each launch issued at the next call
 (environment.DEFER_LAUNCH: no device snapshot of the state the caller has dropped) with one launch
 per step (defer1) or the queued steps fused into launches of up to environment.STEP_BATCH (defer, the
-default); defer_read = defer, reading every step's observation before the next step (a host policy).
+default; defer_all: with every queued step's obs / reward / done stored to the host, not only the
+last's, environment.LIVE_OUTPUTS_ONLY off); defer_read = defer, reading every step's observation
+before the next step (a host policy).
 """
 import os
 import sys
@@ -29,8 +31,9 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 pipe = (sys.argv[2] == "1") if len(sys.argv) > 2 else True
 mode = sys.argv[3] if len(sys.argv) > 3 else "defer"
 environment.ASYNC_STEP = mode != "sync"
-environment.ACTIONS_ZERO_COPY = mode in ("async_zc", "defer1", "defer", "defer_read")
-environment.DEFER_LAUNCH = mode in ("defer1", "defer", "defer_read")
+environment.ACTIONS_ZERO_COPY = mode in ("async_zc", "defer1", "defer", "defer_all", "defer_read")
+environment.DEFER_LAUNCH = mode in ("defer1", "defer", "defer_all", "defer_read")
+environment.LIVE_OUTPUTS_ONLY = mode != "defer_all"
 if mode == "defer1":
     environment.STEP_BATCH = 1
 read = mode == "defer_read"
