@@ -365,6 +365,48 @@ def test_step_batches_match_synchronous_steps(require_gpu, keep, wrapped):
         environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = saved
 
 
+def test_dropped_states_get_no_host_rows(require_gpu):
+    """LIVE_OUTPUTS_ONLY: a queue of steps whose states the caller dropped is issued as one launch
+    without trajectory outputs plus a one-step launch that stores the last state's obs / reward /
+    done into host memory; a state the caller kept ends a launch of its own and gets its rows."""
+    from pupperv3_mjx import environment
+    saved = environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.LIVE_OUTPUTS_ONLY
+    acts = np.random.RandomState(19).uniform(-1, 1, size=(6, N, 12)).astype(np.float32)
+    calls = []
+
+    class Spy:
+        def __init__(self, lib):
+            self._lib = lib
+
+        def __getattr__(self, name):
+            fn = getattr(self._lib, name)
+            if name != "pp3_rollout":
+                return fn
+
+            def call(*args):
+                calls.append((int(args[3]), all(a is None or not getattr(a, "value", a) for a in args[4:7])))
+                return fn(*args)
+            return call
+    try:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.LIVE_OUTPUTS_ONLY = True, True, True
+        e = _env()
+        st = e.reset(make_keys(20, N))
+        e._raw = Spy(e._raw)
+        kept = None
+        for t in range(6):
+            st = e.step(st, acts[t])
+            if t == 2:
+                kept = st
+        _ = st.obs
+        # steps 0-1 (dropped): no outputs; step 2 (kept): its own launch with rows; steps 3-4
+        # (dropped): no outputs; step 5: its own launch with rows
+        assert calls == [(2, True), (1, False), (2, True), (1, False)], calls
+        assert np.isfinite(kept.obs).all() and np.isfinite(st.obs).all()
+        e.close()
+    finally:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.LIVE_OUTPUTS_ONLY = saved
+
+
 def test_step_queue_mixed_with_rollout_branch_and_reset(require_gpu):
     """The step queue (DEFER_LAUNCH, STEP_BATCH) between other calls: a rollout() from the queued
     tail, a step from an older kept state (a branch: the queue is issued, the old state re-uploaded
