@@ -2743,11 +2743,24 @@ void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::Lds
 #define PP3_ACT_PREFETCH 0
 #endif
 
+// PP3_AB_ALIAS (timing probe only, tools/occ_probe.py): both halves of a wave share ONE env block
+// in LDS -- correct only when the wave's two envs are identical (same reset key, actions, no DR), as
+// the probe sets them up -- so a wave needs half the LDS and the occupancy a register budget of
+// PP3_AB_WPE waves per SIMD allows can be timed on the real step code
+#ifndef PP3_AB_ALIAS
+#define PP3_AB_ALIAS 0
+#endif
+#if PP3_AB_ALIAS
+#define PP3_STEP_WPE PP3_AB_WPE
+#else
+#define PP3_STEP_WPE 2
+#endif
 template <int NC, bool FUSED, int NWV = 1>
-__global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
+__global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     typename std::conditional<(NWV > 1), PolicyStepArgs, StepArgs>::type a_arg) {
   static_assert(NWV == 1 || (FUSED && NWV == pp3pol::NWAVE), "the policy rollout is fused, one MLP tile per workgroup");
-  __shared__ Shared<NC> sh[2 * NWV];
+  constexpr bool alias = PP3_AB_ALIAS && NWV == 1;
+  __shared__ Shared<NC> sh[alias ? 1 : 2 * NWV];
   static_assert(NWV == 1 || sizeof(sh) >= pp3pol::TILE_BUF_BYTES, "the MLP's LDS scratch aliases the envs' blocks");
   // the policy rollout's observation tile (its own LDS, next to the env blocks): each env step
   // writes its env's new observation row into it, the next step's MLP reads it in place
@@ -2819,7 +2832,7 @@ __global__ __launch_bounds__(WAVE * NWV, 2) void env_step_kernel(
   if (FUSED) asm volatile("" : "+v"(lane));
   const int wv = NWV > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;  // this wave in the workgroup
   const int h = lane >> 5, l = lane & (HW - 1);
-  Shared<NC>& s = sh[2 * wv + h];
+  Shared<NC>& s = sh[alias ? 0 : 2 * wv + h];
   const int env_raw = 2 * (blockIdx.x * NWV + wv) + h;
   const bool own = env_raw < a.N;
   const int env = own ? env_raw : a.N - 1;

@@ -117,6 +117,10 @@ STEP_BATCH = 16
 # and each row is 1.2 MB of PCIe stores at 4096 envs.  The steps before are one launch without
 # trajectory outputs, the last a launch of its own (bit-equal: a fused launch equals single steps)
 LIVE_OUTPUTS_ONLY = True
+# cap on one queued batch's page-locked output block ([B][N][36H + 2] floats): the batch length B is
+# STEP_BATCH or fewer, so that ASYNC_DEPTH + 1 such blocks stay within a few hundred MB of page-locked
+# memory at long observation histories (H = 20 at 4096 envs: 11.8 MB per step row)
+STEP_BLOCK_MAX_BYTES = 64 << 20
 
 
 def _ro(a):
@@ -177,15 +181,35 @@ class DeviceState(State):
             self._materialize()
         object.__setattr__(self, name, value)
 
+    def __copy__(self):
+        """A shallow copy sharing this state's arrays.  The original is read in full first (its step
+        issued, its outputs waited for, its lazy fields downloaded), so the copy depends on nothing
+        the env later overwrites."""
+        self._materialize()
+        c = object.__new__(type(self))
+        c.__dict__.update(self.__dict__)
+        return c
+
     def _wait_outputs(self) -> None:
         """obs / reward / done of a state whose launch may still run (or still be queued): issue it,
         wait for its completion event, then view the page-locked block the launch stored them into."""
         ready = self.__dict__.get("_ready")
         if ready is None:
             return
-        self._env._flush_for(self)
         if isinstance(ready[0], _StepBatch):  # step j of a batch (STEP_BATCH)
             batch, j = ready
+            # a batch still queued is issued now, whether or not this very object is one of its
+            # tracked states (a shallow copy of a queued state carries the same _ready)
+            if batch is self._env._qb:
+                self._env._flush()
+            if batch.error is not None:
+                raise RuntimeError("the launch of this state's step failed") from batch.error
+            if not batch.stored[j]:
+                # the row was never written: this state's step ended no launch because every state
+                # that could read it had been dropped when the queue was issued (e.g. a copy made
+                # of a state that was then dropped); its outputs are gone, not stale
+                raise RuntimeError("DeviceState: this step's obs/reward/done were not kept (the state it "
+                                   "was copied from was dropped before its step was issued)")
             batch.slot.wait()
             obs, rew, done = batch.views(j, self._single)
         else:
@@ -691,7 +715,7 @@ class PupperV3Env:
         single = _single_of(state)
         act = np.asarray(action, dtype=np.float32).reshape(self.num_envs, _abi.NU)
         qb = self._qb
-        if qb is not None and (qb.n >= max(1, STEP_BATCH) or qb.tail() is not state):
+        if qb is not None and (qb.n >= qb.cap or qb.tail() is not state):
             self._flush()
             qb = None
         if qb is None:
@@ -701,7 +725,7 @@ class PupperV3Env:
             slot = self._act_ring[self._act_i]
             self._act_i = (self._act_i + 1) % len(self._act_ring)
             slot.wait()
-            n, D, B = self.num_envs, self.observation_size, max(1, STEP_BATCH)
+            n, D, B = self.num_envs, self.observation_size, self._step_batch_len()
             lease = _lib.PinnedBlock.take(4 * B * n * (D + 2), self._batch_pool)
             if not self._batch_spares:
                 # a step loop cycles through ASYNC_DEPTH + 1 output blocks (the batch in flight, the
@@ -719,11 +743,17 @@ class PupperV3Env:
         qb.n += 1
         return st
 
-    def _flush_for(self, st: "DeviceState") -> None:
-        """Issue the queued steps if `st` is one of them (its outputs are wanted)."""
-        qb = self._qb
-        if qb is not None and any(r() is st for r in qb.states):
-            self._flush()
+    def _step_batch_len(self) -> int:
+        """Steps per queued batch: STEP_BATCH, fewer where its output block would exceed
+        STEP_BLOCK_MAX_BYTES."""
+        row = 4 * self.num_envs * (self.observation_size + 2)
+        return max(1, min(max(1, STEP_BATCH), STEP_BLOCK_MAX_BYTES // row))
+
+    def flush(self) -> None:
+        """Issue the steps step() has queued (DEFER_LAUNCH) onto the env's stream.  Needed only by
+        callers that read the device buffers (device_field pointers) outside the library after a
+        host-API step: the library's own calls and every State field read issue the queue first."""
+        self._flush()
 
     def _flush(self) -> None:
         """Issue the steps queued by DEFER_LAUNCH (no-op when none are): fused pp3_rollout launches
@@ -735,7 +765,7 @@ class PupperV3Env:
         qb = self._qb
         if qb is None:
             return
-        self._qb = None
+        self._qb = None  # (detached first: _before_launch and the library calls below flush again)
         if qb.n == 0:
             return
         n, D, B = self.num_envs, self.observation_size, qb.cap
@@ -743,19 +773,25 @@ class PupperV3Env:
         act_dev = qb.slot.block.device_ptr()
         ends = [j for j, r in enumerate(qb.states) if j == qb.n - 1 or r() is not None]
         start = 0
-        for e in ends:
-            self._before_launch()
-            if LIVE_OUTPUTS_ONLY and e > start:  # steps start .. e-1: dropped states, no host rows
-                _lib.check(self._raw.pp3_rollout(self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU,
-                                                 e - start, None, None, None, None))
-                start = e
-            _lib.check(self._raw.pp3_rollout(
-                self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU, e - start + 1,
-                C.c_void_p(dev + 4 * (B * n * D + start * n)), C.c_void_p(dev + 4 * (B * n * (D + 1) + start * n)),
-                C.c_void_p(dev + 4 * start * n * D), None))
-            self._gen = qb.gen0 + e + 1
-            self._issued = qb.states[e]
-            start = e + 1
+        try:
+            for e in ends:
+                self._before_launch()
+                if LIVE_OUTPUTS_ONLY and e > start:  # steps start .. e-1: dropped states, no host rows
+                    _lib.check(self._raw.pp3_rollout(self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU),
+                                                     n * _abi.NU, e - start, None, None, None, None))
+                    start = e
+                _lib.check(self._raw.pp3_rollout(
+                    self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU, e - start + 1,
+                    C.c_void_p(dev + 4 * (B * n * D + start * n)), C.c_void_p(dev + 4 * (B * n * (D + 1) + start * n)),
+                    C.c_void_p(dev + 4 * start * n * D), None))
+                for j in range(start if not LIVE_OUTPUTS_ONLY else e, e + 1):
+                    qb.stored[j] = True
+                self._gen = qb.gen0 + e + 1
+                self._issued = qb.states[e]
+                start = e + 1
+        except BaseException as exc:  # the queued states' reads re-raise this instead of viewing unwritten rows
+            qb.error = exc
+            raise
         qb.slot.record()
 
     def rollout(self, state: State, actions) -> Tuple[State, Dict[str, np.ndarray]]:
@@ -1057,6 +1093,8 @@ class _StepBatch:
         self.gen0 = env._gen
         self.states = []  # weak references to the queued states, in order
         self.n = 0
+        self.stored = [False] * cap  # row j's obs / reward / done were stored by an issued launch
+        self.error = None  # the exception an issuing launch raised
 
     def tail(self):
         return self.states[-1]() if self.states else None

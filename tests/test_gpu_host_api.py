@@ -407,6 +407,46 @@ def test_dropped_states_get_no_host_rows(require_gpu):
         environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.LIVE_OUTPUTS_ONLY = saved
 
 
+def test_copies_of_queued_states_and_unstored_rows(require_gpu):
+    """Copies and restores of queued states (advisor r05): copy.copy of a queued state reads its own
+    step's outputs even after the original is dropped; an object restored from a queued state's
+    __dict__ whose original was dropped before the queue was issued raises instead of viewing
+    unwritten rows; env.flush() issues the queue so device_field buffers hold the last step."""
+    import copy
+    import gc
+    acts = np.random.RandomState(23).uniform(-1, 1, size=(5, N, 12)).astype(np.float32)
+    e, ref = _env(), _env()
+    try:
+        st, sr = e.reset(make_keys(21, N)), ref.reset(make_keys(21, N))
+        want = []
+        for t in range(5):
+            sr = ref.step(sr, acts[t])
+            want.append((np.array(sr.obs), np.array(sr.reward)))
+        st = e.step(st, acts[0])
+        st = e.step(st, acts[1])
+        c = copy.copy(st)  # a copy of the queued step 1
+        st = e.step(st, acts[2])
+        restored = object.__new__(type(st))
+        restored.__dict__.update(st.__dict__)  # (bypasses __copy__: untracked by the queue)
+        st = e.step(st, acts[3])
+        st = e.step(st, acts[4])
+        gc.collect()
+        np.testing.assert_array_equal(c.obs, want[1][0])
+        np.testing.assert_array_equal(c.reward, want[1][1])
+        with pytest.raises(RuntimeError, match="not kept"):
+            _ = restored.obs
+        e.flush()
+        assert e._qb is None
+        np.testing.assert_array_equal(st.obs, want[4][0])
+        ptr, n = e.device_field(_abi.F_REWARD)
+        e.synchronize()
+        got = e._get(_abi.F_REWARD, raw=True).reshape(-1)
+        np.testing.assert_array_equal(got, want[4][1])
+    finally:
+        e.close()
+        ref.close()
+
+
 def test_step_queue_mixed_with_rollout_branch_and_reset(require_gpu):
     """The step queue (DEFER_LAUNCH, STEP_BATCH) between other calls: a rollout() from the queued
     tail, a step from an older kept state (a branch: the queue is issued, the old state re-uploaded
