@@ -161,7 +161,8 @@ def ls_cap_stats(env, recs, obs, acts, ids, dr_table=None, terrain=None, converg
         m = env.sys_model.struct if terrain is None else O.model_with_terrain(env.sys_model.struct, terrain[i])
         return O.with_ls_iterations(m, iters) if iters else m
 
-    counts = {p: {"searches": 0, "evals": 0, "converged": 0, "capped": 0, "stalled": 0} for p in ("f64", "f32")}
+    counts = {p: {"searches": 0, "evals": 0, "converged": 0, "capped": 0, "stalled": 0, "bracketing": 0,
+                  "capped_one_sided": 0, "capped_bracketing": 0} for p in ("f64", "f32")}
     counts["f64_converged_run"] = {"searches": 0, "capped": 0, "stalled": 0}
     capped_env = []
     dq, dv, rq = [], [], []
@@ -202,6 +203,12 @@ def ls_cap_stats(env, recs, obs, acts, ids, dr_table=None, terrain=None, converg
             "frac_capped": frac(counts["f64"], "capped"), "frac_stalled": frac(counts["f64"], "stalled"),
             "frac_converged": frac(counts["f64"], "converged"),
             "frac_capped_f32": frac(counts["f32"], "capped"),
+            # where the capped searches ended: the one-sided Newton phase returns its last point (it
+            # depends only on the one-sided exit), the bracketing phase the better end of the bracket
+            # (it depends on updateBracket's candidate rules as restated): DESIGN.md 5
+            "capped_one_sided": frac(counts["f64"], "capped_one_sided"),
+            "capped_bracketing": frac(counts["f64"], "capped_bracketing"),
+            "frac_reaching_bracketing": frac(counts["f64"], "bracketing"),
             "evals_per_search": round(counts["f64"]["evals"] / max(counts["f64"]["searches"], 1), 3),
             "frac_env_steps_with_a_capped_search": round(float(np.mean(capped_env)), 4),
             "counts": counts,

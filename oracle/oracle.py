@@ -123,11 +123,16 @@ def ls_take(precision: str = "f64") -> dict:
     """Line-search counters of this thread since the last call (pp3_oracle.c orc_ls_take): Newton
     searches, their evaluations, the warm-start choice, and how each search ended -- converged
     (ls_converged), capped (ls_iterations evaluations spent first: the alpha then comes from the
-    PrimalSearch exit rule, which MuJoCo's documentation does not specify) or stalled."""
-    out = (C.c_long * 7)()
+    PrimalSearch exit rule, which MuJoCo's documentation does not specify) or stalled; of the capped,
+    those capped in the bracketing phase (`capped_bracketing`; the rest, `capped_one_sided`, ran out
+    in the one-sided Newton phase), and how many searches reached the bracketing phase at all."""
+    out = (C.c_long * 9)()
     lib(precision).orc_ls_take(out)
-    keys = ("evals", "searches", "smooth_starts", "starts", "converged", "capped", "stalled")
-    return dict(zip(keys, (int(v) for v in out)))
+    keys = ("evals", "searches", "smooth_starts", "starts", "converged", "capped", "stalled", "bracketing",
+            "capped_bracketing")
+    d = dict(zip(keys, (int(v) for v in out)))
+    d["capped_one_sided"] = d["capped"] - d["capped_bracketing"]
+    return d
 
 
 def with_ls_iterations(model, n):

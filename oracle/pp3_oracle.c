@@ -1017,6 +1017,9 @@ static _Thread_local long g_ls_total = 0, g_ls_calls = 0, g_ls_smooth = 0, g_ls_
  * it); LS_STALLED = the bracket stopped shrinking (no candidate closer to the root on either side) */
 enum { LS_CONVERGED = 0, LS_CAPPED = 1, LS_STALLED = 2 };
 static _Thread_local long g_ls_exit[3] = {0, 0, 0};
+/* of the searches: those that reached the bracketing phase, and those capped there (the rest of
+ * LS_CAPPED ended in the one-sided phase, whose exit returns the last Newton point unexamined) */
+static _Thread_local long g_ls_bracket = 0, g_ls_cap_bracket = 0;
 static int ls_converged(const LSPoint* p, real gtol) {
   if (RFABS(p->d0) < gtol) return 1;
   return g_ls_noise && RFABS(p->d0) <= LS_NOISE * REPS * p->d1 * RFABS(p->alpha);
@@ -1042,6 +1045,7 @@ static real line_search(LSCtx* c, real gtol, int maxit) {
   }
   if (c->evals >= maxit) { g_ls_exit[LS_CAPPED]++; return p1.alpha; }
   /* bracket [p2, p1]: p2.d0*dir < 0 < p1.d0*dir */
+  g_ls_bracket++;
   p2n = p1;
   p1n.alpha = p1.alpha - p1.d0 / p1.d1;
   ls_eval(c, &p1n);
@@ -1064,6 +1068,7 @@ static real line_search(LSCtx* c, real gtol, int maxit) {
     if (up2) { p2n.alpha = p2.alpha - p2.d0 / p2.d1; ls_eval(c, &p2n); }
   }
   g_ls_exit[c->evals >= maxit ? LS_CAPPED : LS_STALLED]++;
+  g_ls_cap_bracket += c->evals >= maxit;
   return p1.cost < p2.cost ? p1.alpha : p2.alpha;
 }
 
@@ -1771,8 +1776,10 @@ void orc_set_ls_trace(int on) { g_ls_trace = on; }
 void orc_ls_take(long* out) {
   out[0] = g_ls_total; out[1] = g_ls_calls; out[2] = g_ls_smooth; out[3] = g_ls_starts;
   out[4] = g_ls_exit[LS_CONVERGED]; out[5] = g_ls_exit[LS_CAPPED]; out[6] = g_ls_exit[LS_STALLED];
+  out[7] = g_ls_bracket; out[8] = g_ls_cap_bracket;
   g_ls_total = 0; g_ls_calls = 0; g_ls_smooth = 0; g_ls_starts = 0;
   g_ls_exit[0] = g_ls_exit[1] = g_ls_exit[2] = 0;
+  g_ls_bracket = 0; g_ls_cap_bracket = 0;
 }
 void orc_debug_read(double* out) { memcpy(out, g_dbg, sizeof(g_dbg)); }
 int orc_boundary_take(void) { const int n = g_boundary; g_boundary = 0; return n; }

@@ -41,23 +41,6 @@ constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + HW - 1) / HW;
 constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
 constexpr int NHIT = 64;        // contact-overflow ranking window (hits kept for ranking)
 constexpr float LS_NOISE = 64.0f;  // line-search convergence floor, in roundoffs of alpha (oracle LS_NOISE)
-// PP3_LS_E0: the line search's first evaluation (alpha = 0) summed together with the search
-// direction's quadratics (bitwise equal, +0.3 % fused; 0 = after them, as an evaluation of its own)
-#ifndef PP3_LS_E0
-#define PP3_LS_E0 1
-#endif
-// PP3_COM_BF (default 1): the com / cinert / cdof phase as one straight-line block (com_pos): +1.2 %
-// fused.  Not bitwise equal to the branchy form: the backend fuses the rotated inertia's products
-// into FMAs differently in the two blocks (tools/diag_combf.py: com identical, R I R' differs in
-// the last bit on some lanes); GPU suite and one-step error vs the fp64 oracle unchanged
-// (profiles/AB_LOG.md round 5)
-#ifndef PP3_COM_BF
-#define PP3_COM_BF 1
-#endif
-// PP3_PIPE_V2: the pipeline record from flattened sensor records and one LDS round (write_pipeline)
-#ifndef PP3_PIPE_V2
-#define PP3_PIPE_V2 1
-#endif
 
 // Phase-local scratch that never lives across a phase boundary it does not own.
 template <int NC>
@@ -170,14 +153,9 @@ __device__ __forceinline__ float dpp_shr4(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, true));
 }
 
-// wave priority by load (env_step_kernel): contact-weight thresholds (contacts of the busier env
-// of the wave, +2 on the leg-leg Newton path) for the upper priority pair / the top priority
-#ifndef PP3_HEAVY
-#define PP3_HEAVY 5
-#endif
-#ifndef PP3_HEAVY2
-#define PP3_HEAVY2 100
-#endif
+// wave priority by load (env_step_kernel): the contact weight (contacts of the busier env of the
+// wave, +2 on the leg-leg Newton path) from which a wave takes the upper priority pair
+constexpr int HEAVY_WEIGHT = 5;
 
 // ---------------------------- half-wave primitives ----------------------------
 // value of lane k of this lane's half (k compile-time or wave-uniform)
@@ -388,12 +366,12 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
 // Phase 2: subtree com, cinert (mju_inertCom), cdof, robot geom and foot-site positions.
 // lanes 1..13 bodies, 14..31 dofs; then lanes 0..7 geoms, 16..19 feet.
 // ------------------------------------------------------------------------------------
-#if PP3_COM_BF
 // Straight-line form: every lane runs every part (clamped indices; results selected, stores in
 // lane branches at the end), with all LDS operands in one pinned round.  What does not need the
 // subtree com -- the bodies' rotated inertias, the geom / site positions, the base rotation's
-// columns -- then issues while the com's four half-wave sums run, instead of behind them.  The
-// same operations on the same operands as the branchy form below (bitwise equal).
+// columns -- then issues while the com's four half-wave sums run, instead of behind them (+1.2 %
+// against the round-4 branchy form, whose results it matches except for the FMA contraction of the
+// rotated inertia R I R', which differs in the last bit on some lanes: profiles/AB_LOG.md round 5).
 template <int NC>
 __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h, const LaneRec<2>& rc) {
   const bool body = l >= 1 && l < NB;
@@ -490,45 +468,6 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
       cd[3 + k] = d < 3 ? (k == d ? 1.0f : 0.0f) : c[k];
     }
   }
-#if defined(PP3_DEBUG) && defined(PP3_COM_CHECK)
-  {  // diagnostic: the branchy form's values from the same LDS words, compared bit for bit
-    auto miss = [&](int slot, float a, float b) {
-      if (__float_as_uint(a) != __float_as_uint(b)) atomicAdd(&g_dbg[100 + slot], 1.0f);
-    };
-    float mb_ = 0, mx_ = 0, my_ = 0, mz_ = 0;
-    if (body) { mb_ = s.mass[l]; mx_ = mb_ * s.x.xipos[l][0]; my_ = mb_ * s.x.xipos[l][1]; mz_ = mb_ * s.x.xipos[l][2]; }
-    mb_ = hsum(mb_, h); mx_ = hsum(mx_, h); my_ = hsum(my_, h); mz_ = hsum(mz_, h);
-    float co[3];
-    if (mb_ > MINVAL) { const float im = 1.0f / mb_; co[0] = mx_ * im; co[1] = my_ * im; co[2] = mz_ * im; }
-    else { co[0] = s.x.xipos[1][0]; co[1] = s.x.xipos[1][1]; co[2] = s.x.xipos[1][2]; }
-    for (int k = 0; k < 3; k++) miss(k, co[k], com[k]);
-    if (body) {
-      float iq[4], R[9];
-      const float biq[4] = {rc.f[LC_IQUAT], rc.f[LC_IQUAT + 1], rc.f[LC_IQUAT + 2], rc.f[LC_IQUAT + 3]};
-      mulquat(iq, s.xquat[b], biq);
-      quat2mat(iq, R);
-      const float* I2 = s.inertia[b];
-      float A2[3][3];
-      for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++)
-          A2[i][j] = R[3 * i] * I2[0] * R[3 * j] + R[3 * i + 1] * I2[1] * R[3 * j + 1] + R[3 * i + 2] * I2[2] * R[3 * j + 2];
-      const float mm = s.mass[b];
-      const float dx = s.x.xipos[b][0] - co[0], dy = s.x.xipos[b][1] - co[1], dz = s.x.xipos[b][2] - co[2];
-      float c2[10];
-      c2[0] = A2[0][0] + mm * (dy * dy + dz * dz);
-      c2[1] = A2[1][1] + mm * (dx * dx + dz * dz);
-      c2[2] = A2[2][2] + mm * (dx * dx + dy * dy);
-      c2[3] = A2[0][1] - mm * dx * dy;
-      c2[4] = A2[0][2] - mm * dx * dz;
-      c2[5] = A2[1][2] - mm * dy * dz;
-      c2[6] = mm * dx; c2[7] = mm * dy; c2[8] = mm * dz;
-      c2[9] = mm;
-      for (int k = 0; k < 10; k++) miss(3 + k, c2[k], ci[k]);
-      for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) miss(30 + 3 * i + j, A2[i][j], A[i][j]);
-    }
-  }
-#endif
   if (body)
 #pragma unroll
     for (int k = 0; k < 10; k++) s.cinert[b][k] = ci[k];
@@ -548,110 +487,6 @@ __device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l,
     for (int k = 0; k < 3; k++) dst[k] = gpos[k];
   }
 }
-#else
-template <int NC>
-__device__ __forceinline__ void com_pos(Shared<NC>& s, const DevModel& m, int l, int h, const LaneRec<2>& rc) {
-  const bool body = l >= 1 && l < NB;
-  float mb = 0, mx = 0, my = 0, mz = 0;
-  if (body) {
-    mb = s.mass[l];
-    mx = mb * s.x.xipos[l][0];
-    my = mb * s.x.xipos[l][1];
-    mz = mb * s.x.xipos[l][2];
-  }
-  mb = hsum(mb, h);
-  mx = hsum(mx, h);
-  my = hsum(my, h);
-  mz = hsum(mz, h);
-  float com[3];
-  if (mb > MINVAL) { const float im = 1.0f / mb; com[0] = mx * im; com[1] = my * im; com[2] = mz * im; }
-  else { com[0] = s.x.xipos[1][0]; com[1] = s.x.xipos[1][1]; com[2] = s.x.xipos[1][2]; }
-  if (l == 0) { s.com[0] = com[0]; s.com[1] = com[1]; s.com[2] = com[2]; }
-  float ci[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) ci[k] = 0.0f;
-  if (body) {
-    const int b = l;
-    float iq[4], R[9];
-    const float biq[4] = {rc.f[LC_IQUAT], rc.f[LC_IQUAT + 1], rc.f[LC_IQUAT + 2], rc.f[LC_IQUAT + 3]};
-    mulquat(iq, s.xquat[b], biq);
-    quat2mat(iq, R);
-    const float* I = s.inertia[b];
-    float A[3][3];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++)
-        A[i][j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
-    const float mm = s.mass[b];
-    const float dx = s.x.xipos[b][0] - com[0], dy = s.x.xipos[b][1] - com[1], dz = s.x.xipos[b][2] - com[2];
-    ci[0] = A[0][0] + mm * (dy * dy + dz * dz);
-    ci[1] = A[1][1] + mm * (dx * dx + dz * dz);
-    ci[2] = A[2][2] + mm * (dx * dx + dy * dy);
-    ci[3] = A[0][1] - mm * dx * dy;
-    ci[4] = A[0][2] - mm * dx * dz;
-    ci[5] = A[1][2] - mm * dy * dz;
-    ci[6] = mm * dx; ci[7] = mm * dy; ci[8] = mm * dz;
-    ci[9] = mm;
-#pragma unroll
-    for (int k = 0; k < 10; k++) s.cinert[b][k] = ci[k];
-  } else if (l >= 14) {
-    const int d = l - 14;
-    float* cd = s.cdof[d];
-    if (d < 3) {
-      for (int k = 0; k < 6; k++) cd[k] = 0;
-      cd[3 + d] = 1;
-    } else {
-      float ax[3], off[3], c[3];
-      int b;
-      if (d < 6) {  // column d - 3 of the base rotation (3-way selects, not a 9-way register index)
-        float R[9];
-        quat2mat(s.xquat[1], R);
-        const int cc = d - 3;
-        ax[0] = cc == 0 ? R[0] : (cc == 1 ? R[1] : R[2]);
-        ax[1] = cc == 0 ? R[3] : (cc == 1 ? R[4] : R[5]);
-        ax[2] = cc == 0 ? R[6] : (cc == 1 ? R[7] : R[8]);
-        b = 1;
-      } else {
-        const int j = d - 5;
-        ax[0] = s.xaxis[j][0]; ax[1] = s.xaxis[j][1]; ax[2] = s.xaxis[j][2];
-        b = 2 + (d - 6);
-      }
-      for (int k = 0; k < 3; k++) off[k] = com[k] - s.xpos[b][k];
-      cross3(c, ax, off);
-      for (int k = 0; k < 3; k++) { cd[k] = ax[k]; cd[3 + k] = c[k]; }
-    }
-  }
-  // composite inertia of the whole tree (body 1's subtree) for the 6 base dofs
-  {  // all ten sums first (independent DPP chains interleave), then the stores
-    float t[10];
-#pragma unroll
-    for (int k = 0; k < 10; k++) t[k] = hsum_lane16(ci[k]);
-    if (l == 16)
-#pragma unroll
-      for (int k = 0; k < 10; k++) s.crb_base[k] = t[k];
-  }
-  // world positions of the robot collision spheres (lanes 0..7) and foot sites (16..19)
-  const bool geom = l < m.nrobot_geom, foot = l >= 16 && l < 20;
-  if (geom || foot) {
-    const int b = as_i(rc.f[LC_PT_BODY]);
-    const float lp[3] = {rc.f[LC_PT_POS], rc.f[LC_PT_POS + 1], rc.f[LC_PT_POS + 2]};
-    // the body's frame in one pinned round (the stores below may alias it for the compiler, which
-    // otherwise re-reads each position word after the previous store)
-    float q[4], xb[3];
-#pragma unroll
-    for (int k = 0; k < 4; k++) q[k] = s.xquat[b][k];
-#pragma unroll
-    for (int k = 0; k < 3; k++) xb[k] = s.xpos[b][k];
-    PIN("+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(xb[0]), "+v"(xb[1]), "+v"(xb[2]));
-    float R[9], off[3];
-    quat2mat(q, R);
-    matvec(off, R, lp);
-    float* dst = geom ? s.gxpos[l] : s.foot_xpos[l - 16];
-    for (int k = 0; k < 3; k++) dst[k] = xb[k] + off[k];
-  }
-}
-#endif
 
 __device__ __forceinline__ void make_frame(float f[9], const float nin[3]) {
   float a[3] = {nin[0], nin[1], nin[2]};
@@ -2060,7 +1895,6 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
       d0 = t1 + 2.0f * alpha * t2;
       d1 = fmaxf(2.0f * t2, MINVAL);
     };
-#if PP3_LS_E0
     // the first evaluation (alpha = 0) needs nothing the direction's sums produce: its three sums
     // run beside them (six independent DPP chains) instead of after them
     float e0s0, e0s1, e0s2;
@@ -2068,7 +1902,6 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     e0s0 = hsum(e0s0, h);
     e0s1 = hsum(e0s1, h);
     e0s2 = hsum(e0s2, h);
-#endif
     q1 = hsum(q1, h);
     q2 = hsum(q2, h);
     sn = sqrtf(hsum(sn, h));
@@ -2093,11 +1926,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     if (live) {
       const int maxit = m.ls_iterations;
       float c0, g0, h0;
-#if PP3_LS_E0
       finish(0.0f, e0s0, e0s1, e0s2, c0, g0, h0);
-#else
-      eval(0.0f, c0, g0, h0);
-#endif
       evals++;
       float a1 = -g0 / h0, c1, g1, h1;
       eval(a1, c1, g1, h1);
@@ -2392,74 +2221,13 @@ __device__ __forceinline__ void write_obs(Shared<NC>& s, const DevModel& m, cons
   for (int k = l; k < PP3_OBS_DIM; k += HW) obs_out[k] = s.x.e.o[k];
 }
 
-// mjData.sensordata for site sensor i (lane i) from the last forward: mj_sensorPos/Vel/Acc with
-// mj_objectVelocity / mj_objectAcceleration, cacc by mj_rnePostConstraint's recursion along the
-// site body's path (oracle/pp3_oracle.c sensors() is the same restatement).  s.efc_aref holds
-// the forward's qvel (stashed before integration).
-template <int NC>
-__device__ __forceinline__ void sensor_eval(const Shared<NC>& s, const DevModel& m, int i, float* out) {
-  const int sid = m.sensor_objid[i], b = m.site_body[sid], typ = m.sensor_type[i];
-  const float* qv = s.efc_aref;
-  float xq[4] = {s.xquat[b][0], s.xquat[b][1], s.xquat[b][2], s.xquat[b][3]};
-  float Rb[9], sq[4], R[9], sx[3], off[3], dif[3], cr[3], vang[3], vlin[3], v[4] = {0, 0, 0, 0};
-  quat2mat(xq, Rb);
-  matvec(off, Rb, m.site_pos[sid]);
-  for (int k = 0; k < 3; k++) sx[k] = s.xpos[b][k] + off[k];
-  mulquat(sq, xq, m.site_quat[sid]);
-  quat2mat(sq, R);
-  for (int k = 0; k < 3; k++) { dif[k] = sx[k] - s.com[k]; vang[k] = s.cvel[b][k]; }
-  cross3(cr, dif, vang);
-  for (int k = 0; k < 3; k++) vlin[k] = s.cvel[b][3 + k] - cr[k];
-  int dim = 3;
-  if (typ == PP3_SENS_FRAMEPOS) { for (int k = 0; k < 3; k++) v[k] = sx[k]; }
-  else if (typ == PP3_SENS_FRAMEQUAT) { for (int k = 0; k < 4; k++) v[k] = sq[k]; dim = 4; }
-  else if (typ == PP3_SENS_FRAMELINVEL) { for (int k = 0; k < 3; k++) v[k] = vlin[k]; }
-  else if (typ == PP3_SENS_FRAMEANGVEL) { for (int k = 0; k < 3; k++) v[k] = vang[k]; }
-  else if (typ == PP3_SENS_GYRO || typ == PP3_SENS_VELOCIMETER) {
-    const float* w = typ == PP3_SENS_GYRO ? vang : vlin;
-    for (int k = 0; k < 3; k++) v[k] = R[k] * w[0] + R[3 + k] * w[1] + R[6 + k] * w[2];
-  } else if (typ == PP3_SENS_ACCELEROMETER) {
-    int chain[NB], n = 0;
-    for (int bb = b; bb > 0 && n < NB; bb = m.body_parent[bb]) chain[n++] = bb;
-    float ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
-    for (int c = n - 1; c >= 0; c--) {
-      const int bb = chain[c], d0 = m.body_dofadr[bb], nd = m.body_dofnum[bb];
-      float pv[6] = {0, 0, 0, 0, 0, 0};  // velocity the body's dof_dot terms see (parent, + free translation)
-      const int pb = m.body_parent[bb];
-      if (pb > 0)
-        for (int k = 0; k < 6; k++) pv[k] = s.cvel[pb][k];
-      if (nd == 6)
-        for (int d = d0; d < d0 + 3; d++)
-          for (int k = 0; k < 6; k++) pv[k] += s.cdof[d][k] * qv[d];
-      float t1[6] = {0, 0, 0, 0, 0, 0}, t2[6] = {0, 0, 0, 0, 0, 0};
-      for (int d = d0; d < d0 + nd; d++) {
-        float cdd[6] = {0, 0, 0, 0, 0, 0};
-        if (!(nd == 6 && d < d0 + 3)) cross_motion(cdd, pv, s.cdof[d]);
-        for (int k = 0; k < 6; k++) { t1[k] += cdd[k] * qv[d]; t2[k] += s.cdof[d][k] * s.qacc[d]; }
-      }
-      for (int k = 0; k < 6; k++) ca[k] = ca[k] + t1[k] + t2[k];
-    }
-    float aang[3] = {ca[0], ca[1], ca[2]}, alin[3], wl[3], vl[3], c2[3];
-    cross3(cr, dif, aang);
-    for (int k = 0; k < 3; k++) alin[k] = ca[3 + k] - cr[k];
-    for (int k = 0; k < 3; k++) {
-      v[k] = R[k] * alin[0] + R[3 + k] * alin[1] + R[6 + k] * alin[2];
-      wl[k] = R[k] * vang[0] + R[3 + k] * vang[1] + R[6 + k] * vang[2];
-      vl[k] = R[k] * vlin[0] + R[3 + k] * vlin[1] + R[6 + k] * vlin[2];
-    }
-    cross3(c2, wl, vl);
-    for (int k = 0; k < 3; k++) v[k] += c2[k];
-  }
-  const float co = m.sensor_cutoff[i];
-  if (co > 0 && typ != PP3_SENS_FRAMEQUAT)
-    for (int k = 0; k < 3; k++) v[k] = fminf(fmaxf(v[k], -co), co);
-  for (int k = 0; k < dim; k++) out[m.sensor_adr[i] + k] = v[k];
-}
-
-#if PP3_PIPE_V2
-// Sensor lane l (< nsensor) from its host-flattened record (LS_*): the same operations as
-// sensor_eval below, with every model word fetched in one round instead of the dependent
-// lane-indexed loads (sensor -> site -> body -> chain), and the frame's LDS operands pinned.
+// mjData.sensordata from the last forward: mj_sensorPos/Vel/Acc with mj_objectVelocity /
+// mj_objectAcceleration, cacc by mj_rnePostConstraint's recursion along the site body's path
+// (oracle/pp3_oracle.c sensors() is the same restatement).  s.efc_aref holds the forward's qvel
+// (stashed before integration).
+// Sensor lane l (< nsensor) from its host-flattened record (LS_*): every model word fetched in one
+// round instead of dependent lane-indexed loads (sensor -> site -> body -> chain), and the frame's
+// LDS operands pinned.
 template <int NC>
 __device__ __forceinline__ void sensor_eval_rec(const Shared<NC>& s, const DevModel& m, const LaneRec<(LS_WORDS + 3) / 4>& r,
                                                 float* out) {
@@ -2607,36 +2375,6 @@ __device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m,
   if (l < m.nsensor) sensor_eval_rec(s, m, rsens, p + PP3_P_SENSOR);
   for (int i = PP3_P_SENSOR + m.nsensordata + l; i < PP3_PIPE_STRIDE; i += HW) p[i] = 0.0f;
 }
-#else
-template <int NC>
-__device__ __forceinline__ void write_pipeline(Shared<NC>& s, const DevModel& m, float* p, int l, bool = true) {
-  for (int i = l; i < PP3_PIPE_STRIDE; i += HW) {
-    float v = 0.0f;
-    if (i < PP3_P_XQUAT) { const int b = 1 + i / 3, k = i % 3; v = s.xpos[b][k]; }
-    else if (i < PP3_P_XD_VEL) { const int q = i - PP3_P_XQUAT, b = 1 + q / 4, k = q % 4; v = s.xquat[b][k]; }
-    else if (i < PP3_P_XD_ANG) {
-      const int q = i - PP3_P_XD_VEL, b = 1 + q / 3, k = q % 3;
-      const float off[3] = {s.xpos[b][0] - s.com[0], s.xpos[b][1] - s.com[1], s.xpos[b][2] - s.com[2]};
-      float cr[3];
-      cross3(cr, s.cvel[b], off);
-      v = s.cvel[b][3 + k] + cr[k];
-    } else if (i < PP3_P_SITE_XPOS) { const int q = i - PP3_P_XD_ANG, b = 1 + q / 3, k = q % 3; v = s.cvel[b][k]; }
-    else if (i < PP3_P_QFRC_ACT) { const int q = i - PP3_P_SITE_XPOS, f = q / 3, k = q % 3; v = s.foot_xpos[f][k]; }
-    else if (i < PP3_P_QACC) v = s.qfrc_act[i - PP3_P_QFRC_ACT];
-    else if (i < PP3_P_NCON) v = s.qacc[i - PP3_P_QACC];
-    else if (i == PP3_P_NCON) v = (float)s.ncon;
-    else if (i == PP3_P_NHIT) v = (float)s.nhit;
-    else if (i < PP3_P_CON_GEOM) { const int c = i - PP3_P_CON_DIST; v = c < s.ncon ? s.con_dist[c] : 0.0f; }
-    else if (i < PP3_P_SUBTREE_COM) {
-      const int q = i - PP3_P_CON_GEOM, c = q / 2;
-      if (c < s.ncon) { const int pp = s.con_pair[c]; v = (float)m.cg_id[(q & 1) ? m.pair_g2[pp] : m.pair_g1[pp]]; }
-    } else if (i < PP3_P_SUBTREE_COM + 3) v = s.com[i - PP3_P_SUBTREE_COM];
-    else if (i >= PP3_P_SENSOR && i < PP3_P_SENSOR + m.nsensordata) continue;  // written below
-    p[i] = v;
-  }
-  if (l < m.nsensor) sensor_eval(s, m, l, p + PP3_P_SENSOR);
-}
-#endif
 
 // ------------------------------------------------------------------------------------
 // kernels: workgroup b = one wave = envs 2b (lanes 0..31) and 2b+1 (lanes 32..63).  With an
@@ -2677,71 +2415,37 @@ struct PolicyStepArgs {
   pp3pol::Net net;  // the policy (device weight pointers)
 };
 
-// The policy's MLP on this workgroup's tile, out of line (PP3_MLP_NOINLINE, the default): its
-// registers are allocated on their own instead of shaping the env step's allocation around it
-// (inlined, the fused kernel spilled 17 VGPRs; the step alone spills none).
-#ifndef PP3_MLP_PF
-#define PP3_MLP_PF 0  // (measured: one-chunk-ahead prefetch +3 us per step)
-#endif
-#ifndef PP3_MLP_NOINLINE
-#define PP3_MLP_NOINLINE 1
-#endif
-#ifndef PP3_MLP_CG
-#define PP3_MLP_CG 4
-#endif
-#if PP3_MLP_NOINLINE
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-void policy_mlp(pp3pol::KNet* net, const float* obs, int obs_stride, float* act, int n, int row0,
-                pp3pol::LdsTileBuf* buf) {
-  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf, pp3pol::TileRows, PP3_MLP_CG>(
+// The policy's MLP on this workgroup's tile, out of line: its registers are allocated on their own
+// instead of shaping the env step's allocation around it (inlined, the fused kernel spilled 17
+// VGPRs).  Weight chunks of MLP_CG k-groups, no prefetch (chunks of 2 / 8 and a one-chunk-ahead
+// prefetch measured neutral to slower: profiles/AB_LOG.md rounds 4-5).
+constexpr int MLP_CG = 4;
+__device__ __noinline__ void policy_mlp(pp3pol::KNet* net, const float* obs, int obs_stride, float* act, int n,
+                                        int row0, pp3pol::LdsTileBuf* buf) {
+  pp3pol::mlp_tile<pp3pol::KNet, pp3pol::LdsTileBuf, pp3pol::TileRows, MLP_CG>(
       *net, obs, obs_stride, act, NU, n, row0, *buf, threadIdx.x);
 }
 // The same with the observation rows already in the workgroup's LDS tile (observation_history
 // <= 2: 36H <= OBS_TILE_W - 4 floats per row), written by the env steps themselves
 constexpr int OBS_TILE_W = 2 * PP3_OBS_DIM + 4;
 typedef __attribute__((address_space(3))) float LdsObsTile[pp3pol::TILE][OBS_TILE_W];
-#if PP3_MLP_NOINLINE
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::LdsTileBuf* buf, LdsObsTile* in) {
-  pp3pol::mlp_tile<pp3pol::KNet, PP3_MLP_PF != 0, pp3pol::LdsTileBuf, LdsObsTile, PP3_MLP_CG>(
+__device__ __noinline__ void policy_mlp_tile(pp3pol::KNet* net, float* act, int n, int row0, pp3pol::LdsTileBuf* buf,
+                                             LdsObsTile* in) {
+  pp3pol::mlp_tile<pp3pol::KNet, pp3pol::LdsTileBuf, LdsObsTile, MLP_CG>(
       *net, nullptr, 0, act, NU, n, row0, *buf, threadIdx.x, in);
 }
-#ifndef PP3_MLP_OBS_LDS
-#define PP3_MLP_OBS_LDS 1
-#endif
 // Between the fused steps every global value a wave reads back was stored by a wave of the same
-// workgroup (the env step: by the same lane), so on the same CU.  PP3_STEP_ACQ_AGENT=1 (the
-// round-3 form) acquires at agent scope (buffer_inv sc1: the whole vector L1 dropped every step);
-// 0 (default) at workgroup scope, which the gfx942/950 memory model (non-tgsplit) serves from the
-// CU's own L1 without an invalidate: equal end states, +0.4 % on the env rollout, and the policy
-// rollout's three per-step acquires cost 35 us per step at agent scope.
-#ifndef PP3_STEP_ACQ_AGENT
-#define PP3_STEP_ACQ_AGENT 0
-#endif
-#if PP3_STEP_ACQ_AGENT
-#define PP3_STEP_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
-#else
+// workgroup (the env step: by the same lane), so on the same CU: the acquire is at workgroup scope,
+// which the gfx942/950 memory model (non-tgsplit) serves from the CU's own L1 without an invalidate
+// (agent scope -- buffer_inv sc1, the whole vector L1 dropped every step -- measured 0.4 % slower on
+// the env rollout and 35 us per step slower on the policy rollout: profiles/AB_LOG.md round 4).
 #define PP3_STEP_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
-#endif
 
-// Fused rollout, steps after the first: PP3_FUSED_CARRY (default 1: bitwise equal, +0.6 % over 200 fused
-// steps and +0.7 % at the driver's window, profiles/AB_LOG.md round 5) keeps what the previous step left
-// in the env's LDS block instead of reading it back from global memory -- the state record head
-// (s.st is what was stored), the per-env parameters (load_params) and, with observation_history 2,
-// the history frame (the previous step's newest observation, s.x.e.o); PP3_ACT_PREFETCH issues
-// the next step's action load in the epilogue, after its last global-load wait (measured -0.3 %: off).
-#ifndef PP3_FUSED_CARRY
-#define PP3_FUSED_CARRY 1
-#endif
-#ifndef PP3_ACT_PREFETCH
-#define PP3_ACT_PREFETCH 0
-#endif
+// Fused rollout, steps after the first: the wave keeps what the previous step left in the env's LDS
+// block instead of reading it back from global memory (bitwise equal, +0.6 % over 200 fused steps,
+// +0.7 % at the driver's window: profiles/AB_LOG.md round 5) -- the state record head (s.st is what
+// was stored), the per-env parameters (load_params) and, with observation_history 2, the history
+// frame (the previous step's newest observation, s.x.e.o).
 
 // PP3_AB_ALIAS (timing probe only, tools/occ_probe.py): both halves of a wave share ONE env block
 // in LDS -- correct only when the wave's two envs are identical (same reset key, actions, no DR), as
@@ -2782,7 +2486,6 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
   // the loop and kept live across it (SGPR and VGPR spills).  With FUSED false the loop runs once
   // and the kernel compiles to the single-step code it always was.
   int heavy_prev = 0;  // fused: the load flag carries over into the next step's first substep
-  float act_next = 0.0f;  // PP3_ACT_PREFETCH: this lane's action of the next fused step
   for (int it = 0;;) {
 #ifdef PP3_PHASE_PROF
   if (it == 1) pf->n = 0;  // fused launch: the stamp trace holds the second step (a warm one)
@@ -2801,7 +2504,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     typedef __attribute__((address_space(4))) const PolicyStepArgs GPArgs;
     const GPArgs& pa = *(const GPArgs*)ap;
     const int Hm = ((const DevModel*)(const GModel*)a.m)->H;
-    const bool tile_in = PP3_MLP_OBS_LDS && PP3_OBS_DIM * Hm + 4 <= OBS_TILE_W;
+    const bool tile_in = PP3_OBS_DIM * Hm + 4 <= OBS_TILE_W;
     if (tile_in && it == 0) {  // first step of the launch: the observations come from global memory
       for (int i = threadIdx.x; i < pp3pol::TILE * PP3_OBS_DIM * Hm; i += WAVE * NWV) {
         const int r = i / (PP3_OBS_DIM * Hm), k = i - r * (PP3_OBS_DIM * Hm);
@@ -2809,14 +2512,9 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
         obs_tile[r][k] = row < a.N ? a.obs_out[(size_t)row * (PP3_OBS_DIM * Hm) + k] : 0.0f;
       }
     }
-#ifndef PP3_MLP_SKIP
-#define PP3_MLP_SKIP 0  // timing diagnostics only: 1 = no MLP (barriers kept), 2 = no MLP, no barriers
-#endif
-    if (PP3_MLP_SKIP < 2) {
-      __syncthreads();
-      PP3_STEP_ACQUIRE();
-    }
-    if (PP3_MLP_SKIP == 0) {
+    __syncthreads();
+    PP3_STEP_ACQUIRE();
+    {
       if (tile_in)
         policy_mlp_tile(&pa.net, pa.act + (size_t)it * a.act_stride, a.N, blockIdx.x * pp3pol::TILE,
                         (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)), (LdsObsTile*)obs_tile);
@@ -2824,8 +2522,6 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
         policy_mlp(&pa.net, a.obs_out, PP3_OBS_DIM * Hm, pa.act + (size_t)it * a.act_stride, a.N,
                    blockIdx.x * pp3pol::TILE, (pp3pol::LdsTileBuf*)(reinterpret_cast<pp3pol::TileBuf*>(sh)));
       PP3_STEP_ACQUIRE();
-    } else if (PP3_MLP_SKIP == 1) {
-      __syncthreads();
     }
   }
   int lane = NWV > 1 ? (int)(threadIdx.x & (WAVE - 1)) : (int)threadIdx.x;  // (opaque too: lane masks and LDS addresses are rebuilt where used)
@@ -2856,7 +2552,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
   const float* oi = a.obs_in + obs_base;
   float* oo = a.obs_out + obs_base;
   // fused steps after the first: the env's LDS block still holds what this wave left in it
-  const bool carry = PP3_FUSED_CARRY && FUSED && NWV == 1 && it > 0;
+  const bool carry = FUSED && NWV == 1 && it > 0;
   float arow[PP3_MAX_LAG], irow[PP3_MAX_LAG], act_in = 0.0f;
   {
     const float* ar = gst + PP3_S_ACT_BUF + (l < NU ? l : 0) * m.La;
@@ -2866,10 +2562,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
       arow[q] = (l < NU && q < m.La) ? ar[q] : 0.0f;
       irow[q] = (l < 6 && q < m.Li) ? ir[q] : 0.0f;
     }
-    if (l < NU) {
-      if (PP3_ACT_PREFETCH && FUSED && NWV == 1 && it > 0) act_in = act_next;  // (loaded in the last epilogue)
-      else act_in = act_env[l];
-    }
+    if (l < NU) act_in = act_env[l];
   }
   LaneRec<2> re;  // plain loads (no pin): retired with the batch's first wait
   for (int k = 0; k < 2; k++)
@@ -2908,7 +2601,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
       if (l + HW * t < nmove) {
         oo[PP3_OBS_DIM + l + HW * t] = tmp[t];
         if constexpr (NWV > 1)
-          if (PP3_MLP_OBS_LDS && PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][PP3_OBS_DIM + l + HW * t] = tmp[t];
+          if (PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][PP3_OBS_DIM + l + HW * t] = tmp[t];
         if (TG && to) to[PP3_OBS_DIM + l + HW * t] = tmp[t];
       }
   if (!carry)
@@ -2962,11 +2655,11 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
   uint32_t hwid;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
   const int wslot = (int)(hwid & 1u);
-  int heavy = heavy_prev;  // the previous substep's load was high (1) / very high (2): this wave sets the launch's tail
+  int heavy = heavy_prev;  // the previous substep's load was high: this wave sets the launch's tail
   for (int f = 0; f < n_frames; f++) {
     // the heavy waves (many contacts, leg-leg Newton path) ahead of their partners, which have
     // slack; between equals the two slots alternate
-    const int prio = heavy == 2 ? 3 : 2 * heavy + ((f + wslot) & 1);
+    const int prio = 2 * heavy + ((f + wslot) & 1);
     if (prio == 3) __builtin_amdgcn_s_setprio(3);
     else if (prio == 2) __builtin_amdgcn_s_setprio(2);
     else if (prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -2977,7 +2670,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
     const int wgt = substep<NC, NWV>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
-    heavy = wgt >= PP3_HEAVY2 ? 2 : (wgt >= PP3_HEAVY ? 1 : 0);
+    heavy = wgt >= HEAVY_WEIGHT ? 1 : 0;
   }
   if (n_frames > 0) {  // the last substep's Euler step (the others ran inside the next kinematics)
     const GModel* mp = (const GModel*)(a.m);
@@ -3004,7 +2697,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
       for (int k = l; k < PP3_OBS_DIM; k += HW) {
         oo[k] = s.x.e.o[k];
         if constexpr (NWV > 1)
-          if (PP3_MLP_OBS_LDS && PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][k] = s.x.e.o[k];
+          if (PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][k] = s.x.e.o[k];
         if (TG && to) to[k] = s.x.e.o[k];
       }
   }
@@ -3101,12 +2794,6 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     const v4f kb = reinterpret_cast<const v4f*>(&m.pair_con[cpair])[3];  // knee, body counts (host)
     r_knee = kb[1];
     r_body = kb[2];
-  }
-  if (PP3_ACT_PREFETCH && FUSED && NWV == 1) {  // the next fused step's action: in flight from here on
-    // issued after the knee / body load has been waited for (the memory clobber keeps the load
-    // behind it): a wait for an older load would otherwise also wait for this one
-    asm volatile("" ::"v"(r_knee), "v"(r_body) : "memory");
-    if (it + 1 < nsteps && l < NU) act_next = (a.actions + (size_t)(it + 1) * a.act_stride + (size_t)env * NU)[l];
   }
   r_torq = hsum(r_torq, h);
   r_jacc = hsum(r_jacc, h);
@@ -3224,13 +2911,13 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     for (int i = l; i < PP3_FIRST_STRIDE; i += HW) s.st[PP3_S_QPOS + i] = fs[i];
     const float* fo = a.first_obs + (size_t)env * PP3_OBS_DIM * m.H;
     __threadfence_block();  // the prologue's history stores (other lanes, same addresses) land first
-    if (PP3_FUSED_CARRY && FUSED && NWV == 1)  // the next step's carried history frame (H = 2)
+    if (FUSED && NWV == 1)  // the next step's carried history frame (H = 2)
       for (int i = l; i < PP3_OBS_DIM; i += HW) s.x.e.o[i] = fo[i];
     if (own)
       for (int i = l; i < PP3_OBS_DIM * m.H; i += HW) {
         oo[i] = fo[i];
         if constexpr (NWV > 1)
-          if (PP3_MLP_OBS_LDS && PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][i] = fo[i];
+          if (PP3_OBS_DIM * m.H + 4 <= OBS_TILE_W) obs_tile[2 * wv + h][i] = fo[i];
         if (TG && to) to[i] = fo[i];
       }
   }

@@ -61,14 +61,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // so the layer records are scalar loads)
 typedef __attribute__((address_space(4))) const Net KNet;
 
-#ifndef PP3_MLP_DIAG
-#define PP3_MLP_DIAG 0  // timing diagnostics only (wrong results): 1 identity activations, 2 every chunk
-#endif                  // reads tile 0's first chunk (L1-resident weights), 4 no MFMA, 8 no barriers
 // One chunk (CG groups of 4 k-blocks) of tile t's B fragments, starting at group g0 (groups past
 // ngrp read as zero)
 template <int CG>
 __device__ __forceinline__ void load_chunk(const Layer& L, int t, int g0, int lane, f32x4 (&bq)[CG]) {
-  if (PP3_MLP_DIAG & 2) { t = 0; g0 = 0; }
   const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
 #pragma unroll
   for (int q = 0; q < CG; q++) bq[q] = (g0 + q < L.ngrp) ? wf[(size_t)q * 64] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -88,7 +84,6 @@ __device__ __forceinline__ T* uni(T* p) {
 // the same for a chunk that lies wholly inside the layer (no predicates)
 template <int CG>
 __device__ __forceinline__ void load_chunk_full(const Layer& L, int t, int g0, int lane, f32x4 (&bq)[CG]) {
-  if (PP3_MLP_DIAG & 2) { t = 0; g0 = 0; }
   const f32x4* wf = reinterpret_cast<const f32x4*>(L.w) + ((size_t)t * L.ngrp + g0) * 64 + lane;
 #pragma unroll
   for (int q = 0; q < CG; q++) bq[q] = wf[(size_t)q * 64];
@@ -106,19 +101,15 @@ __device__ __forceinline__ Layer layer_of(NetT& net, int li) {
 // The MLP of observation rows row0 .. row0+15 (rows >= n read as zero, get no action) ->
 // act[row * act_stride + col] for col < out_dim.  Called by all 64 * NWAVE threads of the
 // workgroup (tid = threadIdx.x); `buf` is the workgroup's LDS scratch.  Ends with a barrier.
-// NetT: Net (a kernel's by-value argument) or KNet.  PF (the fused rollout, which has the
-// registers): every weight chunk's loads are issued one chunk ahead -- the next chunk of the
-// tile, else the next tile's first, else the first chunk of this wave's first tile in the next
-// layer, across the epilogue and barrier -- and the very first before the observation tile is
-// staged.  Only the issue points of loads move: the MFMA sequence, and so the result, is the
-// same with and without.  `in` (InT = float[TILE][W] in LDS, W >= in_dim, in_dim a multiple of
+// NetT: Net (a kernel's by-value argument) or KNet.  Weight chunks are loaded where they are
+// multiplied (a one-chunk-ahead prefetch measured slower: profiles/AB_LOG.md).  `in` (InT = float[TILE][W] in LDS, W >= in_dim, in_dim a multiple of
 // 4): the observation rows are already there (written by the env step, a barrier since), so the
 // first layer reads them in place instead of staging `obs` from global memory; rows past n may
 // hold anything (a row's outputs depend on that row only, and they are not stored).
 // CG: groups of 4 k-blocks per chunk (8 in the stand-alone kernel; the fused rollout's out-of-line
 // call uses 4, whose registers fit the callee's caller-saved VGPRs: no save / restore through
 // scratch per call).  The MFMA sequence does not depend on it.
-template <class NetT, bool PF = false, class BufT = TileBuf, class InT = TileRows, int CG = CG8>
+template <class NetT, class BufT = TileBuf, class InT = TileRows, int CG = CG8>
 __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ obs, int obs_stride,
                                          float* __restrict__ act, int act_stride, int n, int row0, BufT& buf,
                                          int tid, InT* in = nullptr) {
@@ -129,11 +120,6 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
   row0 = uni(row0);
   act = uni(act);
   act_stride = uni(act_stride);
-  f32x4 nxt[CG];  // PF: the next chunk's B fragments, in flight
-  if (PF) {
-    const Layer L0 = layer_of(net, 0);
-    if (wave < L0.Mp / TILE) load_chunk(L0, wave, 0, lane, nxt);
-  }
   if (!in) {
     // observation tile -> LDS (rows past n are zero)
     const int kp0 = uni(net.layer[0].Kp), in_dim = uni(net.in_dim);
@@ -147,7 +133,7 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
     __syncthreads();
   }
   // one layer's output tiles of this wave: X the [TILE][.] input rows, Y the output rows
-  auto layer = [&](auto& X, auto& Y, const Layer& L, int li, bool last) {
+  auto layer = [&](auto& X, auto& Y, const Layer& L, bool last) {
     const int ntile = L.Mp / TILE;
     for (int t = wave; t < ntile; t += NWAVE) {
       const int c0 = t * TILE;
@@ -163,19 +149,7 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
         const bool full = g0 + CG <= L.ngrp && 4 * (g0 + CG) <= nblk;
         f32x4 bq[CG];
         float av[CG][4];
-        if (PF) {
-#pragma unroll
-          for (int q = 0; q < CG; q++) bq[q] = nxt[q];
-          // the next chunk: this tile's, the next tile's of this layer, or the next layer's first
-          if (g0 + CG < L.ngrp) {
-            load_chunk(L, t, g0 + CG, lane, nxt);
-          } else if (t + NWAVE < ntile) {
-            load_chunk(L, t + NWAVE, 0, lane, nxt);
-          } else if (!last) {
-            const Layer Ln = layer_of(net, li + 1);
-            if (wave < Ln.Mp / TILE) load_chunk(Ln, wave, 0, lane, nxt);
-          }
-        } else if (full) {
+        if (full) {
           load_chunk_full(L, t, g0, lane, bq);
         } else {
           load_chunk(L, t, g0, lane, bq);  // every load of the chunk in flight together
@@ -196,10 +170,7 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
         }
 #pragma unroll
         for (int q = 0; q < CG; q++) {
-          if (PP3_MLP_DIAG & 4) {
-            acc[0] += av[q][0] * bq[q].x + av[q][2] * bq[q].z;
-            acc1[0] += av[q][1] * bq[q].y + av[q][3] * bq[q].w;
-          } else if (full || g0 + q < L.ngrp) {  // uniform; padded blocks of a ragged group multiply zeros
+          if (full || g0 + q < L.ngrp) {  // uniform; padded blocks of a ragged group multiply zeros
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][0], bq[q].x, acc, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][1], bq[q].y, acc1, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q][2], bq[q].z, acc, 0, 0, 0);
@@ -211,7 +182,7 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = 4 * (lane >> 4) + r;
-        const float v = (PP3_MLP_DIAG & 1) ? acc[r] + bias : activate(acc[r] + bias, L.act);
+        const float v = activate(acc[r] + bias, L.act);
         if (!last) {
           Y[row][col] = v;
         } else if (col < L.M && row0 + row < n) {
@@ -219,15 +190,15 @@ __device__ __forceinline__ void mlp_tile(NetT& net, const float* __restrict__ ob
         }
       }
     }
-    if (!(PP3_MLP_DIAG & 8)) __syncthreads();
+    __syncthreads();
   };
   int cur = 0;
   const int n_layers = uni(net.n_layers);
   for (int li = 0; li < n_layers; li++) {
     const Layer L = layer_of(net, li);
     const bool last = li == n_layers - 1;
-    if (li == 0 && in) layer(*in, buf[1], L, li, last);
-    else layer(buf[cur], buf[cur ^ 1], L, li, last);
+    if (li == 0 && in) layer(*in, buf[1], L, last);
+    else layer(buf[cur], buf[cur ^ 1], L, last);
     cur ^= 1;
   }
 }

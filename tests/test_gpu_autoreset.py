@@ -36,8 +36,11 @@ def _oracle_wrapped_step(oe, rec, obs, action, ep, prev_done, first_state, first
     return out_rec, out_obs, float(done), ep_new, o
 
 
-@pytest.mark.parametrize("episode_length,terminal_z", [(7, 0.1), (1000, 0.3)])
-def test_auto_reset_episode_semantics(require_gpu, tmp_path, episode_length, terminal_z):
+@pytest.mark.parametrize("episode_length,terminal_z,nsteps", [(7, 0.1, 16), (1000, 0.3, 16), (1000, 0.12, 40)])
+def test_auto_reset_episode_semantics(require_gpu, tmp_path, episode_length, terminal_z, nsteps):
+    """(7, 0.1): truncations; (1000, 0.3): every env terminates at every step (terminal height above
+    every start height), so only the reset path is compared; (1000, 0.12): terminations mixed with
+    surviving envs, whose obs / reward are compared on the non-done path (at least 50 env steps)."""
     path = common.write_model(tmp_path, 0)
     n = 8
     e = PupperV3Env(**common.fixture_kwargs(path, terminal_body_z=terminal_z), num_envs=n)
@@ -53,7 +56,7 @@ def test_auto_reset_episode_semantics(require_gpu, tmp_path, episode_length, ter
         rs = np.random.RandomState(5)
         n_done = n_trunc = 0
         fb = G.FlipBudget()
-        for t in range(16):
+        for t in range(nsteps):
             a = rs.uniform(-1, 1, size=(n, 12)).astype(np.float32)
             prev = st
             ep_prev = e._get(_abi.F_EPISODE)
@@ -81,6 +84,8 @@ def test_auto_reset_episode_semantics(require_gpu, tmp_path, episode_length, ter
         assert n_done > 0
         if episode_length == 7:
             assert n_trunc > 0
+        if terminal_z < 0.2:  # the robots survive some steps: the non-done path is compared
+            assert fb.n >= 50, fb.n
     finally:
         e.close()
 

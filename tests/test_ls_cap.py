@@ -51,6 +51,10 @@ def test_cap_binds_on_the_sliding_ball():
         assert r["c5"]["converged"] + r["c5"]["capped"] + r["c5"]["stalled"] == 1
         assert r["c50"]["capped"] == 0  # 50 evaluations always suffice here
         assert r["c5"]["evals"] <= 5 + 2  # the bracket loop may finish its round (p1next / p2next)
+        # the capped searches split by the phase they ran out in (bench ls_cap)
+        c = r["c5"]
+        assert c["capped_one_sided"] + c["capped_bracketing"] == c["capped"]
+        assert c["capped_one_sided"] >= 0 and c["capped_bracketing"] <= c["bracketing"] <= c["searches"]
     assert len(capped) >= 4 and len(free) >= 2, [r["c5"] for r in rows]
     # a capped search returns a different step: by up to tens of m/s^2 on this contact
     assert max(r["dqacc"] for r in capped) > 10.0
