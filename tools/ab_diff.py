@@ -16,8 +16,12 @@ a = _lib.DeviceBuffer(K * E * 48, 0)
 _lib.check(env._L.pp3_fill_uniform(env._h, a.ptr, K * E * 12, 1234, 0, -1.0, 1.0, None))
 out = [env._get(_abi.F_STATE)]
 pipes = []
+FUSED = os.environ.get("AB_DIFF_FUSED") == "1"  # one fused rollout launch per step (the fused kernel)
 for i in range(K):
-    env.step_device(a.ptr.value + i * E * 48)
+    if FUSED:
+        env.rollout_device(a.ptr.value + i * E * 48, E * 12, 2 if i == 0 else 1)  # (nsteps 1 takes the single-step kernel)
+    else:
+        env.step_device(a.ptr.value + i * E * 48)
     env.synchronize()
     out.append(env._get(_abi.F_STATE)); pipes.append(env._get(_abi.F_PIPELINE))
 np.savez(sys.argv[1], states=np.array(out), pipes=np.array(pipes))
