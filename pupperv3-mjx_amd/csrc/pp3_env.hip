@@ -633,8 +633,6 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const v4f& pc0, int
   s.con_mu[slot] = s.dr_on ? mu_dr : mu_model;
 }
 
-template <int NC, int NWV>
-__device__ __forceinline__ int collision_finish(Shared<NC>& s, const DevModel& m, int l, int h, int nhit, const TerrainRef& tr);
 // Phase 3a: collision (mj_collision), contacts compacted in pair order; when more than
 // NC pairs penetrate, the NC deepest are kept (same rule as the oracle).  Returns lane c's
 // contact support (pair_sup of contact c; 4 = no contact): the Newton phases read contact
@@ -658,12 +656,6 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
     }
     nhit += __popc(mask);
   }
-  return collision_finish<NC, NWV>(s, m, l, h, nhit, tr);
-}
-// the end of the collision pass: contact counts, the overflow ranking (keep the NC deepest) and
-// lane c's contact support
-template <int NC, int NWV>
-__device__ __forceinline__ int collision_finish(Shared<NC>& s, const DevModel& m, int l, int h, int nhit, const TerrainRef& tr) {
   if (l == 0) { s.nhit = nhit; s.ncon = nhit < NC ? nhit : NC; }
   const bool ovf = nhit > NC;
   if (__ballot(ovf)) {  // rare: keep the NC deepest among the first NHIT hits, in pair order
@@ -821,168 +813,6 @@ __device__ __forceinline__ void crb_times_cdof(Shared<NC>& s, const DevModel& m,
   mul_inert_vec(s.x.a.F[l], crb, cdv);
 }
 
-
-#ifdef PP3_AB_XBRANCH
-// A/B (verdict r05 item 2): the CRB x cdof rows, the RNE velocity chain and the first batch of the
-// narrow phase as ONE straight-line block -- every lane evaluates all three on clamped indices
-// (the plane-sphere and sphere-sphere distances both, selected by pair kind; sphere-box pairs keep
-// their branch after the block), every LDS operand in one pinned round, the stores at the end --
-// so the collision branch's loads and arithmetic issue under the CRB / RNE chains and vice versa.
-// Then the collision's compaction, as collision() (later pair batches and the overflow ranking
-// unchanged).
-template <int NC, int NWV = 1>
-__device__ __forceinline__ int crb_rne_collision(Shared<NC>& s, const DevModel& m, int l, int h, const PairLoad& pre) {
-  // ---- operands ----
-  const int lc = l < NV ? l : NV - 1;
-  const bool base = lc < 6;
-  const int b = base ? 2 : lc - 4, last = 2 + 3 * ((b - 2) / 3) + 2;
-  const int b1 = b + 1 <= last ? b + 1 : b, b2 = b + 2 <= last ? b + 2 : b;
-  const float* r0 = base ? s.crb_base : s.cinert[b];
-  float crb[10], c1[10], c2[10], cdv[6];
-#pragma unroll
-  for (int k = 0; k < 10; k++) { crb[k] = r0[k]; c1[k] = s.cinert[b1][k]; c2[k] = s.cinert[b2][k]; }
-#pragma unroll
-  for (int k = 0; k < 6; k++) cdv[k] = s.cdof[lc][k];
-  const int lr = l & 3;
-  float lcd[3][6], lqd[3], bcd[3][6], bq[6];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const int d = 6 + 3 * lr + k;
-#pragma unroll
-    for (int c = 0; c < 6; c++) lcd[k][c] = s.cdof[d][c];
-    lqd[k] = s.qvel[d];
-  }
-#pragma unroll
-  for (int d = 0; d < 3; d++)
-#pragma unroll
-    for (int k = 0; k < 6; k++) bcd[d][k] = s.cdof[3 + d][k];
-#pragma unroll
-  for (int k = 0; k < 6; k++) bq[k] = s.qvel[k];
-  PairLoad pl = pre;
-  PIN("+v"(pl.v[0]), "+v"(pl.v[1]), "+v"(pl.v[2]), "+v"(pl.v[3]), "+v"(pl.v[4]), "+v"(pl.v[5]), "+v"(pl.v[6]));
-  PairRec rec;
-  __builtin_memcpy(&rec, pl.v, sizeof(rec));
-  const v4f pc0 = pl.v[6];
-  const int i1 = rec.s1 >= 0 ? rec.s1 : 0, i2 = rec.s2 >= 0 ? rec.s2 : 0;
-  float g1[3], g2[3];
-#pragma unroll
-  for (int k = 0; k < 3; k++) { g1[k] = s.gxpos[i1][k]; g2[k] = s.gxpos[i2][k]; }
-  PIN("+v"(crb[0]), "+v"(crb[1]), "+v"(crb[2]), "+v"(crb[3]), "+v"(crb[4]), "+v"(crb[5]), "+v"(crb[6]), "+v"(crb[7]),
-      "+v"(crb[8]), "+v"(crb[9]), "+v"(cdv[0]), "+v"(cdv[1]), "+v"(cdv[2]), "+v"(cdv[3]), "+v"(cdv[4]), "+v"(cdv[5]));
-  PIN("+v"(c1[0]), "+v"(c1[1]), "+v"(c1[2]), "+v"(c1[3]), "+v"(c1[4]), "+v"(c1[5]), "+v"(c1[6]), "+v"(c1[7]),
-      "+v"(c1[8]), "+v"(c1[9]), "+v"(c2[0]), "+v"(c2[1]), "+v"(c2[2]), "+v"(c2[3]), "+v"(c2[4]), "+v"(c2[5]),
-      "+v"(c2[6]), "+v"(c2[7]), "+v"(c2[8]), "+v"(c2[9]));
-  PIN("+v"(lcd[0][0]), "+v"(lcd[0][1]), "+v"(lcd[0][2]), "+v"(lcd[0][3]), "+v"(lcd[0][4]), "+v"(lcd[0][5]),
-      "+v"(lcd[1][0]), "+v"(lcd[1][1]), "+v"(lcd[1][2]), "+v"(lcd[1][3]), "+v"(lcd[1][4]), "+v"(lcd[1][5]),
-      "+v"(lcd[2][0]), "+v"(lcd[2][1]), "+v"(lcd[2][2]), "+v"(lcd[2][3]), "+v"(lcd[2][4]), "+v"(lcd[2][5]),
-      "+v"(lqd[0]), "+v"(lqd[1]), "+v"(lqd[2]));
-  PIN("+v"(bcd[0][0]), "+v"(bcd[0][1]), "+v"(bcd[0][2]), "+v"(bcd[0][3]), "+v"(bcd[0][4]), "+v"(bcd[0][5]),
-      "+v"(bcd[1][0]), "+v"(bcd[1][1]), "+v"(bcd[1][2]), "+v"(bcd[1][3]), "+v"(bcd[1][4]), "+v"(bcd[1][5]),
-      "+v"(bcd[2][0]), "+v"(bcd[2][1]), "+v"(bcd[2][2]), "+v"(bcd[2][3]), "+v"(bcd[2][4]), "+v"(bcd[2][5]),
-      "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(bq[4]), "+v"(bq[5]));
-  PIN("+v"(g1[0]), "+v"(g1[1]), "+v"(g1[2]), "+v"(g2[0]), "+v"(g2[1]), "+v"(g2[2]));
-  // ---- CRB x cdof (lanes < NV) ----
-  const float w1 = (!base && b + 1 <= last) ? 1.0f : 0.0f, w2 = (!base && b + 2 <= last) ? 1.0f : 0.0f;
-#pragma unroll
-  for (int k = 0; k < 10; k++) crb[k] += w1 * c1[k];
-#pragma unroll
-  for (int k = 0; k < 10; k++) crb[k] += w2 * c2[k];
-  float F[6];
-  mul_inert_vec(F, crb, cdv);
-  // ---- RNE chain (lanes 0..3: base -> leg lr) ----
-  float w[3] = {0, 0, 0}, bsum[3] = {0, 0, 0};
-#pragma unroll
-  for (int d = 0; d < 3; d++) {
-    const float q = bq[3 + d];
-#pragma unroll
-    for (int k = 0; k < 3; k++) { w[k] += bcd[d][k] * q; bsum[k] += bcd[d][3 + k] * q; }
-  }
-  const float v0 = bq[0], v1 = bq[1], v2 = bq[2];
-  float cv[6] = {w[0], w[1], w[2], v0 + bsum[0], v1 + bsum[1], v2 + bsum[2]};
-  float ca[6] = {0, 0, 0, -m.gravity[0] + (v1 * w[2] - v2 * w[1]), -m.gravity[1] + (v2 * w[0] - v0 * w[2]),
-                 -m.gravity[2] + (v0 * w[1] - v1 * w[0])};
-  float cv0[6], ca0[6], cvl[3][6], cal[3][6];
-#pragma unroll
-  for (int c = 0; c < 6; c++) { cv0[c] = cv[c]; ca0[c] = ca[c]; }
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    float cdd[6];
-    cross_motion(cdd, cv, lcd[k]);
-    const float qd = lqd[k];
-#pragma unroll
-    for (int c = 0; c < 6; c++) { cv[c] += lcd[k][c] * qd; ca[c] += cdd[c] * qd; }
-#pragma unroll
-    for (int c = 0; c < 6; c++) { cvl[k][c] = cv[c]; cal[k][c] = ca[c]; }
-  }
-  // ---- narrow phase, first pair batch: plane-sphere and sphere-sphere, selected ----
-  const int p = l;
-  float p1[3], p2[3];
-#pragma unroll
-  for (int k = 0; k < 3; k++) { p1[k] = rec.s1 >= 0 ? g1[k] : rec.p1[k]; p2[k] = rec.s2 >= 0 ? g2[k] : rec.p2[k]; }
-  const float vv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
-  float dist, pos[3], nrm[3];
-  {
-    const float nz[3] = {rec.R[2], rec.R[5], rec.R[8]};
-    const float dps = dot3(nz, vv) - rec.r2;
-    const float len = sqrtf(dot3(vv, vv));
-    const float dss = len - rec.r1 - rec.r2;
-    float nss[3];
-    if (len < MINVAL) { nss[0] = 1; nss[1] = 0; nss[2] = 0; }
-    else { const float il = 1.0f / len; nss[0] = vv[0] * il; nss[1] = vv[1] * il; nss[2] = vv[2] * il; }
-    const bool ps = rec.kind == PK_PLANE_SPHERE;
-    dist = ps ? dps : dss;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const float pps = p2[k] - nz[k] * (rec.r2 + 0.5f * dps);
-      const float pss = p1[k] + nss[k] * (rec.r1 + 0.5f * dss);
-      nrm[k] = ps ? nz[k] : nss[k];
-      pos[k] = ps ? pps : pss;
-    }
-  }
-  bool hit = rec.kind != PK_SPHERE_BOX && dist <= rec.margin;
-  // ---- stores ----
-  if (l < NV)
-#pragma unroll
-    for (int k = 0; k < 6; k++) s.x.a.F[l][k] = F[k];
-  if (l == 0)
-#pragma unroll
-    for (int k = 0; k < 6; k++) { s.cvel[1][k] = cv0[k]; s.x.a.cacc[1][k] = ca0[k]; }
-  if (l < 4)
-#pragma unroll
-    for (int k = 0; k < 3; k++)
-#pragma unroll
-      for (int c = 0; c < 6; c++) { s.cvel[2 + 3 * l + k][c] = cvl[k][c]; s.x.a.cacc[2 + 3 * l + k][c] = cal[k][c]; }
-  // ---- collision (as collision()): sphere-box pairs of the first batch, then compaction ----
-  const TerrainRef tr{m.terrain, m.nbox};
-  v4f pcx = pc0;
-  if (rec.kind == PK_SPHERE_BOX) hit = narrow<NC, NWV>(s, tr, pl, dist, pos, nrm, pcx);
-  hit = hit && p < m.npair;
-  int nhit = 0;
-  {
-    const uint32_t mask = hballot(hit, h);
-    const int slot = __popc(mask & ((1u << l) - 1u));
-    if (hit) {
-      if (slot < NC) store_contact(s, pc0, slot, p, dist, pos, nrm);
-      if (slot < NHIT) { s.x.a.hit_dist[slot] = dist; s.x.a.hit_pair[slot] = p; }
-    }
-    nhit = __popc(mask);
-  }
-  for (int bs = HW; bs < m.npair; bs += HW) {
-    const int q = bs + l;
-    float d2 = 0, ps2[3], nr2[3];
-    v4f pcq;
-    const bool hq = narrow<NC, NWV>(s, tr, load_pair(m, q < m.npair ? q : 0), d2, ps2, nr2, pcq) && (q < m.npair);
-    const uint32_t mask = hballot(hq, h);
-    const int slot = nhit + __popc(mask & ((1u << l) - 1u));
-    if (hq) {
-      if (slot < NC) store_contact(s, pcq, slot, q, d2, ps2, nr2);
-      if (slot < NHIT) { s.x.a.hit_dist[slot] = d2; s.x.a.hit_pair[slot] = q; }
-    }
-    nhit += __popc(mask);
-  }
-  return collision_finish<NC, NWV>(s, m, l, h, nhit, tr);
-}
-#endif
 
 // ------------------------------------------------------------------------------------
 // LDL^T in registers: lane i (< NV) of each half holds row i; returns L_ik (k<i) in a[k],
@@ -1595,14 +1425,10 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   // v22: 28 more registers live through kinematics and com)
   const PairLoad pair_pf = load_pair(m, l < m.npair ? l : 0);
   // ---- phase 3: CRB*cdof, RNE chain, collision, actuation/passive, limit + friction rows ----
-  int lsup = 4;  // lane c: support of contact c (4 = none)
-#ifdef PP3_AB_XBRANCH
-  { lsup = crb_rne_collision<NC, NWV>(s, m, l, h, pair_pf); SYNC(); }
-#else
   { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
+  int lsup = 4;  // lane c: support of contact c (4 = none)
   { lsup = collision<NC, NWV>(s, m, l, h, pair_pf); SYNC(); }
-#endif
   PHASE(16); l = opaque_lane(l);
   // the PairCon of contact c = l / 4 for the first batch of phase 13's edge rows (lane e = 4c + k),
   // loaded here unpinned: it arrives during the limit/actuation and M-entry phases
