@@ -492,6 +492,10 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="per-step RCCL hand-over of obs|reward|done to the learner rank (configs[3])")
     ap.add_argument("--gather-root", type=int, default=0, help="learner rank of --gather; -1 = all-gather")
+    ap.add_argument("--gather-mode", choices=("step", "unroll"), default="step",
+                    help="--gather: hand over every step (single-step launches, one pp3_gather each), or the K "
+                         "timed steps as ONE fused rollout whose trajectory is handed over once "
+                         "(pp3_gather_rollout: Brax's generate_unroll + one learner hand-over per unroll)")
     ap.add_argument("--auto-reset", type=int, default=0, metavar="EPISODE_LENGTH",
                     help="on-device EpisodeWrapper+AutoResetWrapper (brax training wrap) with this episode length")
     ap.add_argument("--policy", type=str, default="", metavar="H1,H2,...",
@@ -600,7 +604,8 @@ def main():
         nmax = E  # equal shards: every rank contributes E rows of width 36H + 2
         width = env.observation_size + 2
         if args.gather_root < 0 or rank == args.gather_root:
-            gather_dst = _lib.DeviceBuffer(world * nmax * width * 4, device)
+            per = args.steps if args.gather_mode == "unroll" else 1  # (unroll: [world][K][nmax][width])
+            gather_dst = _lib.DeviceBuffer(world * per * nmax * width * 4, device)
         if comm is None:  # one rank: the gather is a pack (a one-rank communicator still runs it)
             comm = sharding.Comm(0, 1, device, tag="_solo")
 
@@ -625,7 +630,8 @@ def main():
     # --launch rollout (the default for the plain env-step workloads): the timed K steps are one
     # fused launch writing per-step trajectories; the start state is kept to replay the same K
     # steps as single-step launches afterwards (timed, and checked bit-equal)
-    rollout = args.launch == "rollout" and policy is None and not args.gather
+    unroll_gather = args.gather and args.gather_mode == "unroll"
+    rollout = args.launch == "rollout" and policy is None and (not args.gather or unroll_gather)
     traj, snap = None, None
     if rollout or policy is not None:
         D = env.observation_size
@@ -682,10 +688,13 @@ def main():
         _lib.check(L.pp3_rollout_policy_timed(env._h, policy._h, args.steps, C.c_void_p(act_at(args.warmup)),
                                               traj[0].ptr, traj[1].ptr, traj[2].ptr, C.byref(ms)))
         kernel_ms = ms.value
-    elif not args.gather and rollout:
+    elif rollout:
         _lib.check(L.pp3_rollout_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps,
                                        traj[0].ptr, traj[1].ptr, traj[2].ptr, C.byref(ms)))
         kernel_ms = ms.value
+        if unroll_gather:  # the unroll's trajectory to the learner: one collective, on the env stream
+            comm.gather_rollout(env, traj[2].ptr.value, traj[0].ptr.value, traj[1].ptr.value, args.steps, nmax,
+                                gather_dst.ptr.value if gather_dst else None, root=args.gather_root)
     elif not args.gather:
         _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps, C.byref(ms)))
         kernel_ms = ms.value
@@ -752,8 +761,11 @@ def main():
         if not idle_same:
             print(f"rank {rank}: idle-start replay differs from the timed rollout", file=sys.stderr, flush=True)
     if rollout:
-        for b in list(traj) + list(snap.values()):
+        for b in snap.values():
             b.free()
+        if not unroll_gather:  # (the unroll hand-over is timed alone below, on these buffers)
+            for b in traj:
+                b.free()
     if policy is not None:
         # the same K steps again as the unfused loop (per step a pp3_policy_act launch on the obs
         # buffer, then a single-step launch) from the kept start state: actions and end state must
@@ -799,7 +811,7 @@ def main():
     import hashlib
     state_sha16 = hashlib.sha256((end[_abi.F_STATE] if (rollout or policy is not None) else env._get(_abi.F_STATE)).tobytes()).hexdigest()[:16]
     gather_info = None
-    if args.gather:
+    if args.gather and not unroll_gather:
         # untimed: the same K steps' kernels alone (events), then the gather alone
         _lib.check(L.pp3_step_timed(env._h, C.c_void_p(act_at(args.warmup)), E * 12, args.steps, C.byref(ms)))
         kernel_ms = ms.value
@@ -811,9 +823,25 @@ def main():
         env.synchronize()
         barrier()
         gather_s = (time.perf_counter() - tg) / args.steps
-        gather_info = {"root": args.gather_root, "rows_per_rank": nmax, "row_floats": env.observation_size + 2,
-                       "bytes_per_rank": nmax * (env.observation_size + 2) * 4,
+        gather_info = {"mode": "step", "root": args.gather_root, "rows_per_rank": nmax,
+                       "row_floats": env.observation_size + 2, "bytes_per_rank": nmax * (env.observation_size + 2) * 4,
                        "ms_per_gather": round(gather_s * 1e3, 4), "transport": "RCCL (pp3_gather), env stream"}
+    elif unroll_gather:
+        # untimed: the unroll's hand-over alone (the trajectory buffers still hold the timed unroll)
+        env.synchronize()
+        barrier()
+        tg = time.perf_counter()
+        comm.gather_rollout(env, traj[2].ptr.value, traj[0].ptr.value, traj[1].ptr.value, args.steps, nmax,
+                            gather_dst.ptr.value if gather_dst else None, root=args.gather_root)
+        env.synchronize()
+        barrier()
+        gather_s = time.perf_counter() - tg
+        for b in traj:
+            b.free()
+        gather_info = {"mode": "unroll", "root": args.gather_root, "steps_per_gather": args.steps,
+                       "rows_per_rank": args.steps * nmax, "row_floats": env.observation_size + 2,
+                       "bytes_per_rank": args.steps * nmax * (env.observation_size + 2) * 4,
+                       "ms_per_gather": round(gather_s * 1e3, 4), "transport": "RCCL (pp3_gather_rollout), env stream"}
     if comm is not None and comm.world > 1:
         wall_max, kernel_ms_max = (float(v) for v in comm.allreduce([wall, kernel_ms], "max"))
     else:
@@ -883,7 +911,10 @@ def main():
                                        "domain randomisation" if args.dr else "no DR")),
                        "envs_per_gpu": E, "global_envs": E * world, "obs_history": env._observation_history,
                        "n_frames": env._n_frames, "parallelism": f"env-sharded x{world} (no data-path collective)"
-                       if not args.gather else f"env-sharded x{world} + per-step RCCL gather to rank {args.gather_root}",
+                       if not args.gather else (f"env-sharded x{world} + per-step RCCL gather to rank {args.gather_root}"
+                                                if not unroll_gather else
+                                                f"env-sharded x{world} + one RCCL gather of the {args.steps}-step unroll "
+                                                f"to rank {args.gather_root}"),
                        "per_env_terrain": bool(args.terrain),
                        "commands": "reset-sampled, resampled every 500 steps" if args.random_commands else "fixed (0.5,0,0)",
                        "gather": gather_info, "gather_check": gcheck, "comm": comm_kind, "auto_reset_episode_length": args.auto_reset or None,

@@ -537,6 +537,16 @@ const char* pp3_comm_last_error(void);
  * must live on the communicator's device (PP3_ERR_ARG otherwise); the caller's current HIP device
  * is restored on return. */
 int pp3_gather(pp3_comm_t* comm, pp3_env_t* env, int32_t nmax, int32_t root, float* dst_dev, void* stream);
+/* The same hand-over for a K-step unroll (replaces the per-device trajectory of Brax's
+ * generate_unroll, [ext] brax 0.12.1 brax/training/acting.py, that PPO's pmap hands to the learner
+ * once per unroll): the trajectory outputs of one fused pp3_rollout of this env (traj_obs
+ * [nsteps][N][36H], traj_reward / traj_done [nsteps][N], device pointers) -> rank r's block
+ * [nsteps][nmax][36H + 2] at dst_dev + r * nsteps * nmax * (36H + 2); rows past the rank's env
+ * count are zero.  ONE collective per unroll instead of one per step; root, stream and device
+ * rules as pp3_gather. */
+int pp3_gather_rollout(pp3_comm_t* comm, pp3_env_t* env, const float* traj_obs, const float* traj_reward,
+                       const float* traj_done, int32_t nsteps, int32_t nmax, int32_t root, float* dst_dev,
+                       void* stream);
 /* Host-blocking helpers for timing: element-wise sum / max of n <= 64 doubles over ranks, and
  * a barrier. */
 int pp3_comm_allreduce(pp3_comm_t* comm, const double* in, double* out, int32_t n, int32_t op);

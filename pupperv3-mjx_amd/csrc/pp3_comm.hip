@@ -140,16 +140,55 @@ __global__ void pack_kernel(const float* __restrict__ obs, const float* __restri
   out[i] = v;
 }
 
+// the same for a K-step trajectory ([K][n][D] obs, [K][n] reward / done) -> out [K][nmax][D + 2]
+__global__ void pack_traj_kernel(const float* __restrict__ obs, const float* __restrict__ rew,
+                                 const float* __restrict__ done, int n, int D, int nmax, long total,
+                                 float* __restrict__ out) {
+  const int W = D + 2;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long per = (long)nmax * W;
+  const long t = i / per;
+  const long j = i - t * per;
+  const int row = (int)(j / W), c = (int)(j - (long)row * W);
+  float v = 0.0f;
+  if (row < n) {
+    const long r = t * n + row;
+    v = c < D ? obs[r * D + c] : (c == D ? rew[r] : done[r]);
+  }
+  out[i] = v;
+}
+
 }  // namespace
 
 struct pp3_comm {
   int rank, world, device;
   ncclComm_t comm;
   hipStream_t stream;  // host-blocking helpers (barrier, reductions)
-  float* pack;         // [nmax][D+2] staging of this rank's chunk (allgather / non-root)
+  float* pack;         // [nmax][D+2] (or [K][nmax][D+2]) staging of this rank's chunk (allgather / non-root)
   size_t pack_elems;
   double* red;         // reduction scratch
 };
+namespace {
+int exchange(pp3_comm* c, const Rccl* R, float* mine, size_t count, int root, float* dst_dev, hipStream_t s);
+// where this rank's chunk of `count` floats is packed: the root straight into its own slot of the
+// destination, every other rank into the (grown on demand) staging buffer
+int chunk_of(pp3_comm* c, size_t count, int root, float* dst_dev, hipStream_t s, float** mine) {
+  if (root >= 0 && root == c->rank) {
+    *mine = dst_dev + (size_t)c->rank * count;
+    return PP3_OK;
+  }
+  if (c->pack_elems < count) {
+    HCHK(hipStreamSynchronize(s));  // (first call / growth only) the old buffer may be in flight
+    (void)hipFree(c->pack);
+    c->pack = nullptr;
+    HCHK(hipMalloc(&c->pack, count * sizeof(float)));
+    c->pack_elems = count;
+  }
+  *mine = c->pack;
+  return PP3_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -230,24 +269,50 @@ int pp3_gather(pp3_comm_t* c, pp3_env_t* e, int32_t nmax, int32_t root, float* d
   hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)pp3_stream(e);
   DeviceScope dev(c->device);
   HCHK(dev.err);
-  // the root packs straight into its own slot of the destination; every other chunk is staged
   float* mine;
-  if (root >= 0 && root == c->rank) {
-    mine = dst_dev + (size_t)c->rank * count;
-  } else {
-    if (c->pack_elems < count) {
-      HCHK(hipStreamSynchronize(s));  // (first call / growth only) the old buffer may be in flight
-      (void)hipFree(c->pack);
-      c->pack = nullptr;
-      HCHK(hipMalloc(&c->pack, count * sizeof(float)));
-      c->pack_elems = count;
-    }
-    mine = c->pack;
-  }
+  if (const int rc = chunk_of(c, count, root, dst_dev, s, &mine)) return rc;
   const unsigned blocks = (unsigned)((count + 255) / 256);
   hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, s, (const float*)obs, (const float*)rew,
                      (const float*)done, n, (int)D, nmax, mine);
   HCHK(hipGetLastError());
+  return exchange(c, R, mine, count, root, dst_dev, s);
+}
+
+int pp3_gather_rollout(pp3_comm_t* c, pp3_env_t* e, const float* traj_obs, const float* traj_reward,
+                       const float* traj_done, int32_t nsteps, int32_t nmax, int32_t root, float* dst_dev,
+                       void* stream) {
+  if (!c || !e || !traj_obs || !traj_reward || !traj_done) return cerr(PP3_ERR_ARG, "pp3_gather_rollout: null argument");
+  if (nsteps < 1) return cerr(PP3_ERR_ARG, "pp3_gather_rollout: nsteps must be >= 1");
+  if (root >= c->world) return cerr(PP3_ERR_ARG, "pp3_gather_rollout: root out of range");
+  if (pp3_env_device(e) != c->device)
+    return cerr(PP3_ERR_ARG, "pp3_gather_rollout: the env and the communicator are on different devices");
+  const int n = pp3_num_envs(e);
+  if (nmax < n) return cerr(PP3_ERR_ARG, "pp3_gather_rollout: nmax smaller than this rank's shard");
+  if ((root < 0 || root == c->rank) && !dst_dev) return cerr(PP3_ERR_ARG, "pp3_gather_rollout: null destination");
+  const Rccl* R = rccl();
+  if (!R) return cerr(PP3_ERR_COMM, g_cerr);
+  void* obs;
+  int64_t D;
+  if (pp3_field(e, PP3_F_OBS, &obs, &D)) return cerr(PP3_ERR_ARG, std::string("pp3_gather_rollout: ") + pp3_last_error());
+  const size_t W = (size_t)D + 2, count = (size_t)nsteps * nmax * W;
+  hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)pp3_stream(e);
+  DeviceScope dev(c->device);
+  HCHK(dev.err);
+  float* mine;
+  if (const int rc = chunk_of(c, count, root, dst_dev, s, &mine)) return rc;
+  const unsigned blocks = (unsigned)((count + 255) / 256);
+  hipLaunchKernelGGL(pack_traj_kernel, dim3(blocks), dim3(256), 0, s, traj_obs, traj_reward, traj_done, n, (int)D,
+                     nmax, (long)count, mine);
+  HCHK(hipGetLastError());
+  return exchange(c, R, mine, count, root, dst_dev, s);
+}
+
+}  // extern "C"
+
+namespace {
+// the collective of pp3_gather / pp3_gather_rollout: this rank's `count` floats at `mine` (already
+// in its own slot when it is the root) -> rank-major slots of `count` at dst
+int exchange(pp3_comm* c, const Rccl* R, float* mine, size_t count, int root, float* dst_dev, hipStream_t s) {
   if (root < 0) {
     NCHK(R, R->AllGather(mine, dst_dev, count, ncclFloat32, c->comm, s));
   } else if (c->world > 1) {
@@ -266,6 +331,9 @@ int pp3_gather(pp3_comm_t* c, pp3_env_t* e, int32_t nmax, int32_t root, float* d
   }
   return PP3_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int pp3_comm_allreduce(pp3_comm_t* c, const double* in, double* out, int32_t n, int32_t op) {
   if (!c || !in || !out || n < 1 || n > 64) return cerr(PP3_ERR_ARG, "pp3_comm_allreduce: bad argument (n <= 64)");

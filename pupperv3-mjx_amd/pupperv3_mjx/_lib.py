@@ -102,6 +102,7 @@ def load() -> C.CDLL:
     L.pp3_comm_world.restype = i32
     L.pp3_comm_last_error.restype = C.c_char_p
     L.pp3_gather.argtypes = [vp, vp, i32, i32, vp, vp]
+    L.pp3_gather_rollout.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]
     L.pp3_render.argtypes = [i32, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, C.POINTER(C.c_float), vp, vp]
     L.pp3_render_last_error.restype = C.c_char_p
     L.pp3_comm_allreduce.argtypes = [vp, vp, vp, i32, i32]
@@ -113,7 +114,7 @@ def load() -> C.CDLL:
                  "pp3_device_malloc", "pp3_device_free", "pp3_memcpy_h2d", "pp3_memcpy_d2h",
                  "pp3_outputs_to_host", "pp3_host_device_ptr", "pp3_memcpy_d2d", "pp3_fill_uniform", "pp3_step_timed", "pp3_phase_profile",
                  "pp3_wave_profile", "pp3_set_auto_reset", "pp3_set_action_repeat", "pp3_policy_create", "pp3_policy_act", "pp3_policy_destroy", "pp3_rollout_policy",
-                 "pp3_rollout_policy_timed", "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather",
+                 "pp3_rollout_policy_timed", "pp3_set_terrain", "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_gather", "pp3_gather_rollout",
                  "pp3_comm_allreduce", "pp3_comm_barrier", "pp3_render"):
         getattr(L, name).restype = C.c_int
     if L.pp3_abi_version() != _abi.ABI_VERSION:
@@ -148,7 +149,7 @@ EXPORTED_SYMBOLS = (
     "pp3_stream", "pp3_event_create", "pp3_event_record", "pp3_event_synchronize", "pp3_event_destroy",
     "pp3_set_terrain", "pp3_terrain_slots",
     "pp3_comm_unique_id", "pp3_comm_init", "pp3_comm_destroy", "pp3_comm_rank", "pp3_comm_world",
-    "pp3_comm_last_error", "pp3_gather", "pp3_comm_allreduce", "pp3_comm_barrier",
+    "pp3_comm_last_error", "pp3_gather", "pp3_gather_rollout", "pp3_comm_allreduce", "pp3_comm_barrier",
     "pp3_render", "pp3_render_last_error",
 )
 

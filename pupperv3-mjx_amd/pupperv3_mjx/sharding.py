@@ -10,7 +10,9 @@ communicator id is exchanged by a file rendezvous on the node (``rendezvous_id``
 
 Gathered layout (``pp3_gather``): rank r's ``nmax`` rows of width D + 2 at row r * nmax, rows past
 the rank's env count zero; ``pack_rows`` is its numpy statement, ``unpack_gathered`` drops the
-padding and returns the global [G, D] / [G] / [G] batch in env-id order.
+padding and returns the global [G, D] / [G] / [G] batch in env-id order.  For a K-step unroll
+(``Comm.gather_rollout`` -> ``pp3_gather_rollout``: one collective per unroll, the trajectory of one
+fused ``pp3_rollout``) rank r's block is [K][nmax][D + 2] at r * K * nmax rows (``pack_traj_rows``).
 """
 from __future__ import annotations
 
@@ -58,6 +60,13 @@ def pack_rows(obs, reward, done, nmax: int) -> np.ndarray:
     out[:n, D] = np.asarray(reward, dtype=np.float32).reshape(n)
     out[:n, D + 1] = np.asarray(done, dtype=np.float32).reshape(n)
     return out
+
+
+def pack_traj_rows(obs, reward, done, nmax: int) -> np.ndarray:
+    """numpy statement of pp3_comm.hip's pack_traj_kernel: a K-step trajectory (obs [K, n, D], reward
+    / done [K, n]) -> [K, nmax, D + 2], zero rows past the shard's env count."""
+    obs = np.asarray(obs, dtype=np.float32)
+    return np.stack([pack_rows(obs[t], np.asarray(reward)[t], np.asarray(done)[t], nmax) for t in range(obs.shape[0])])
 
 
 def unpack_gathered(full, global_envs: int, world: int):
@@ -195,6 +204,18 @@ class Comm:
         self._lib.check_comm(self._L.pp3_gather(self._h, env._h, int(nmax), int(root),
                                                 C.c_void_p(dst_dev) if dst_dev else None,
                                                 C.c_void_p(stream) if stream else None))
+
+    def gather_rollout(self, env, traj_obs: int, traj_reward: int, traj_done: int, nsteps: int, nmax: int,
+                       dst_dev: Optional[int], root: int = 0, stream: Optional[int] = None) -> None:
+        """The K-step unroll of one fused rollout (device trajectory buffers [K][n][D] / [K][n] /
+        [K][n]) of every rank into dst_dev ([world][K][nmax][D + 2]): one collective per unroll."""
+        if hasattr(env, "_flush"):
+            env._flush()
+        vp = C.c_void_p
+        self._lib.check_comm(self._L.pp3_gather_rollout(self._h, env._h, vp(traj_obs), vp(traj_reward), vp(traj_done),
+                                                        int(nsteps), int(nmax), int(root),
+                                                        vp(dst_dev) if dst_dev else None,
+                                                        vp(stream) if stream else None))
 
     def allreduce(self, values, op: str = "max") -> np.ndarray:
         from . import _abi

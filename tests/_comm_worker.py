@@ -43,6 +43,33 @@ full = np.empty((world * nmax, W), np.float32)
 dst.download(full)
 np.save(os.path.join(out, f"allgather_{rank}.npy"), full)
 comm.barrier()
+# a K-step unroll (one fused rollout writing its trajectory on the device) handed over ONCE
+# (pp3_gather_rollout), to root 0 and to everyone
+K = 3
+D = env.observation_size
+tr = [_lib.DeviceBuffer(K * n * D * 4, env.device), _lib.DeviceBuffer(K * n * 4, env.device),
+      _lib.DeviceBuffer(K * n * 4, env.device)]
+ua = np.random.RandomState(7).uniform(-1, 1, size=(K, G, 12)).astype(np.float32)[:, start:start + n]
+abuf = _lib.DeviceBuffer(ua.nbytes, env.device)
+abuf.upload(np.ascontiguousarray(ua))
+env.rollout_device(abuf.ptr.value, n * 12, K, tr[1].ptr.value, tr[2].ptr.value, tr[0].ptr.value)
+env.synchronize()
+got = [np.empty((K, n, D), np.float32), np.empty((K, n), np.float32), np.empty((K, n), np.float32)]
+for b, a in zip(tr, got):
+    b.download(a)
+np.save(os.path.join(out, f"traj_rows_{rank}.npy"), sharding.pack_traj_rows(got[0], got[1], got[2], nmax))
+tdst = _lib.DeviceBuffer(world * K * nmax * W * 4, env.device)
+for root in (0, -1):
+    comm.gather_rollout(env, tr[0].ptr.value, tr[1].ptr.value, tr[2].ptr.value, K, nmax,
+                        tdst.ptr.value if (root < 0 or rank == 0) else None, root=root)
+    env.synchronize()
+    if root < 0 or rank == 0:
+        full = np.empty((world * K * nmax, W), np.float32)
+        tdst.download(full)
+        np.save(os.path.join(out, f"traj_{'root_0' if root == 0 else 'allgather'}_{rank}.npy"), full)
+    comm.barrier()
+for b in tr + [abuf, tdst]:
+    b.free()
 dst.free()
 env.close()
 comm.close()

@@ -58,6 +58,47 @@ def test_gather_packs_learner_rows(comm, root):
         env.close()
 
 
+@pytest.mark.parametrize("root", [0, -1])
+def test_gather_rollout_packs_the_unroll(comm, root):
+    """pp3_gather_rollout on a one-rank communicator: the K-step trajectory of one fused rollout
+    (device buffers written by pp3_rollout), packed as [K][nmax][D + 2] with zero padding rows, must
+    equal sharding.pack_traj_rows of the same trajectory -- and that trajectory equals K single
+    steps (rollout() is bit-equal to step())."""
+    n, nmax, K = 37, 40, 4
+    env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=n)
+    try:
+        st = env.reset(make_keys(9, n))
+        acts = np.random.RandomState(4).uniform(-1, 1, size=(K, n, 12)).astype(np.float32)
+        D = env.observation_size
+        W = D + 2
+        tr = [_lib.DeviceBuffer(K * n * D * 4, env.device), _lib.DeviceBuffer(K * n * 4, env.device),
+              _lib.DeviceBuffer(K * n * 4, env.device)]
+        abuf = _lib.DeviceBuffer(acts.nbytes, env.device)
+        abuf.upload(acts)
+        env.rollout_device(abuf.ptr.value, n * 12, K, tr[1].ptr.value, tr[2].ptr.value, tr[0].ptr.value)
+        dst = _lib.DeviceBuffer(K * nmax * W * 4, env.device)
+        dst.upload(np.full(K * nmax * W, np.nan, np.float32))
+        comm.gather_rollout(env, tr[0].ptr.value, tr[1].ptr.value, tr[2].ptr.value, K, nmax, dst.ptr.value, root=root)
+        env.synchronize()
+        got = np.empty((K, nmax, W), np.float32)
+        dst.download(got)
+        # the same K steps through the host API (a fresh env from the same keys)
+        e2 = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=n)
+        try:
+            s2 = e2.reset(make_keys(9, n))
+            want = []
+            for t in range(K):
+                s2 = e2.step(s2, acts[t])
+                want.append(sharding.pack_rows(s2.obs, s2.reward, s2.done, nmax))
+        finally:
+            e2.close()
+        np.testing.assert_array_equal(got, np.stack(want))
+        for b in tr + [abuf, dst]:
+            b.free()
+    finally:
+        env.close()
+
+
 def test_gather_rejects_short_nmax(comm):
     env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=8)
     try:
@@ -121,3 +162,9 @@ def test_two_rank_gather_on_two_devices(require_gpu, tmp_path):
         np.testing.assert_array_equal(root[r * nmax:(r + 1) * nmax], mine[r])
         ag = np.load(tmp_path / f"allgather_{r}.npy")
         np.testing.assert_array_equal(ag, np.concatenate(mine))
+    tmine = [np.load(tmp_path / f"traj_rows_{r}.npy") for r in range(2)]
+    K, W = tmine[0].shape[0], tmine[0].shape[2]
+    troot = np.load(tmp_path / "traj_root_0_0.npy").reshape(2, K, nmax, W)
+    for r in range(2):
+        np.testing.assert_array_equal(troot[r], tmine[r])
+        np.testing.assert_array_equal(np.load(tmp_path / f"traj_allgather_{r}.npy").reshape(2, K, nmax, W), troot)

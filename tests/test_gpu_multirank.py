@@ -62,6 +62,13 @@ def test_gather_across_rank_processes(loopback_env, tmp_path, world, G):
         assert mine[r].shape[0] == nmax
         np.testing.assert_array_equal(root[r * nmax:(r + 1) * nmax], mine[r])
         np.testing.assert_array_equal(np.load(tmp_path / f"allgather_{r}.npy"), np.concatenate(mine))
+    # the K-step unroll handed over once (pp3_gather_rollout): rank r's [K][nmax][D + 2] block
+    tmine = [np.load(tmp_path / f"traj_rows_{r}.npy") for r in range(world)]
+    K, W = tmine[0].shape[0], tmine[0].shape[2]
+    troot = np.load(tmp_path / "traj_root_0_0.npy").reshape(world, K, nmax, W)
+    for r in range(world):
+        np.testing.assert_array_equal(troot[r], tmine[r])
+        np.testing.assert_array_equal(np.load(tmp_path / f"traj_allgather_{r}.npy").reshape(world, K, nmax, W), troot)
     # the sharded job reproduces the single-GPU batch env for env
     env = PupperV3Env(**common.fixture_kwargs(common.MODEL_XML), num_envs=G)
     try:
@@ -109,6 +116,21 @@ def test_bench_per_step_gather(loopback_env, root):
     assert d["n_gpus"] == 2
     g = d["config"]["gather"]
     assert g["root"] == root and g["rows_per_rank"] == 512 and g["ms_per_gather"] > 0
+    assert d["config"]["gather_check"]["failing_receivers"] == 0
+
+
+@pytest.mark.parametrize("root", [0, -1])
+def test_bench_unroll_gather(loopback_env, root):
+    """configs[3] with one hand-over per unroll (--gather-mode unroll): the K timed steps are ONE
+    fused rollout and its K-step trajectory goes to the learner rank (or every rank) in one
+    pp3_gather_rollout; the fused launch is still bit-equal to the single-step replay."""
+    d = _bench(loopback_env, "--gpus", "2", "--gather", "--gather-mode", "unroll", "--gather-root", str(root),
+               "--random-commands")
+    assert d["n_gpus"] == 2
+    g = d["config"]["gather"]
+    assert g["mode"] == "unroll" and g["root"] == root and g["steps_per_gather"] == 4
+    assert g["rows_per_rank"] == 4 * 512 and g["ms_per_gather"] > 0
+    assert d["per_step_launch"]["bit_equal_to_rollout"]
     assert d["config"]["gather_check"]["failing_receivers"] == 0
 
 
