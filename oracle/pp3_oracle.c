@@ -1028,48 +1028,50 @@ static int ls_converged(const LSPoint* p, real gtol) {
 /* engine_solver.c PrimalSearch-style exact line search: Newton step from 0, one-sided Newton
  * until the derivative changes sign, then bracketed Newton/midpoint refinement. */
 static real line_search(LSCtx* c, real gtol, int maxit) {
+  /* labels P0 ... B7: DESIGN.md 5 (the branch-by-branch statement, for checking against
+   * engine_solver.c PrimalSearch / updateBracket) */
   LSPoint p0, p1, p2, pmid, p1n, p2n;
   p0.alpha = 0;
-  ls_eval(c, &p0);
+  ls_eval(c, &p0);                                          /* P0 */
   p1.alpha = p0.alpha - p0.d0 / p0.d1;
-  ls_eval(c, &p1);
-  if (p0.cost < p1.cost) p1 = p0;
-  if (ls_converged(&p1, gtol)) { g_ls_exit[LS_CONVERGED]++; return p1.alpha; }
-  real dir = p1.d0 < 0 ? 1 : -1;
+  ls_eval(c, &p1);                                          /* P1 */
+  if (p0.cost < p1.cost) p1 = p0;                           /* P2 */
+  if (ls_converged(&p1, gtol)) { g_ls_exit[LS_CONVERGED]++; return p1.alpha; }  /* P3 */
+  real dir = p1.d0 < 0 ? 1 : -1;                            /* O1 */
   p2 = p1;
-  while (p1.d0 * dir <= -gtol && c->evals < maxit) {
+  while (p1.d0 * dir <= -gtol && c->evals < maxit) {        /* O2 */
     p2 = p1;
     p1.alpha -= p1.d0 / p1.d1;
     ls_eval(c, &p1);
     if (ls_converged(&p1, gtol)) { g_ls_exit[LS_CONVERGED]++; return p1.alpha; }
   }
-  if (c->evals >= maxit) { g_ls_exit[LS_CAPPED]++; return p1.alpha; }
+  if (c->evals >= maxit) { g_ls_exit[LS_CAPPED]++; return p1.alpha; }  /* O3 */
   /* bracket [p2, p1]: p2.d0*dir < 0 < p1.d0*dir */
   g_ls_bracket++;
-  p2n = p1;
+  p2n = p1;                                                 /* B0 */
   p1n.alpha = p1.alpha - p1.d0 / p1.d1;
   ls_eval(c, &p1n);
-  while (c->evals < maxit) {
+  while (c->evals < maxit) {                                /* B1 */
     pmid.alpha = (real)0.5 * (p1.alpha + p2.alpha);
-    ls_eval(c, &pmid);
+    ls_eval(c, &pmid);                                      /* B2 */
     LSPoint cand[3] = {p1n, p2n, pmid};
     int best = -1;
-    for (int i = 0; i < 3; i++)
+    for (int i = 0; i < 3; i++)                             /* B3 */
       if (ls_converged(&cand[i], gtol) && (best < 0 || cand[i].cost < cand[best].cost)) best = i;
     if (best >= 0) { g_ls_exit[LS_CONVERGED]++; return cand[best].alpha; }
     int up1 = 0, up2 = 0;
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < 3; i++) {                           /* B4 */
       /* tighten each bracket end with any candidate on its side that is closer to the root */
       if (p1.d0 * cand[i].d0 > 0 && RFABS(cand[i].d0) < RFABS(p1.d0)) { p1 = cand[i]; up1 = 1; }
       if (p2.d0 * cand[i].d0 > 0 && RFABS(cand[i].d0) < RFABS(p2.d0)) { p2 = cand[i]; up2 = 1; }
     }
-    if (!up1 && !up2) break;
-    if (up1) { p1n.alpha = p1.alpha - p1.d0 / p1.d1; ls_eval(c, &p1n); }
+    if (!up1 && !up2) break;                                /* B5 */
+    if (up1) { p1n.alpha = p1.alpha - p1.d0 / p1.d1; ls_eval(c, &p1n); }  /* B6 */
     if (up2) { p2n.alpha = p2.alpha - p2.d0 / p2.d1; ls_eval(c, &p2n); }
   }
   g_ls_exit[c->evals >= maxit ? LS_CAPPED : LS_STALLED]++;
   g_ls_cap_bracket += c->evals >= maxit;
-  return p1.cost < p2.cost ? p1.alpha : p2.alpha;
+  return p1.cost < p2.cost ? p1.alpha : p2.alpha;           /* B7 */
 }
 
 static void solve_newton(const Model* m, Data* d) {
