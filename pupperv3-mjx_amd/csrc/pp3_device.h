@@ -279,11 +279,47 @@ __device__ __forceinline__ void normalize4(float q[4]) {
   if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
   else { float i = 1.0f / n; q[0] *= i; q[1] *= i; q[2] *= i; q[3] *= i; }
 }
+// sincosf restricted to |x| < 2^17: the device library's own small-argument path, operation for
+// operation (Cody-Waite reduction by pi/2 in three parts, its sin / cos polynomials, the quadrant
+// signs), so the results are bit-identical there (tools/sincos_check.hip) -- without the
+// Payne-Hanek branch for larger arguments, whose dead code and hoisted constants the library call
+// leaves in every caller.  Joint half-angles never come near 2^17 (beyond it the reduction loses
+// accuracy instead); non-finite arguments give NaN as sincosf does.
+__device__ __forceinline__ void sincos_f32(float x, float* sp, float* cp) {
+  const float ax = __builtin_fabsf(x);
+  const float n = __builtin_rintf(ax * 0x1.45f306p-1f);  // x 2/pi
+  const int q = (int)n;
+  float r = __builtin_fmaf(n, -0x1.921fb4p+0f, ax);
+  r = __builtin_fmaf(n, -0x1.4442d0p-24f, r);
+  r = __builtin_fmaf(n, -0x1.846988p-48f, r);
+  const float x2 = r * r;
+  float ps = __builtin_fmaf(-0x1.983304p-13f, x2, 0x1.110388p-7f);
+  ps = __builtin_fmaf(x2, ps, -0x1.55553ap-3f);
+  ps = x2 * ps;
+  const float sr = __builtin_fmaf(r, ps, r);
+  float pc = __builtin_fmaf(0x1.aea668p-16f, x2, -0x1.6c9e76p-10f);
+  pc = __builtin_fmaf(x2, pc, 0x1.5557eep-5f);
+  pc = __builtin_fmaf(x2, pc, -0x1.000008p-1f);
+  const float cr = __builtin_fmaf(x2, pc, 1.0f);
+  const bool odd = (q & 1) != 0;
+  const uint32_t qs = ((uint32_t)q << 30) & 0x80000000u;  // quadrants 2, 3: both signs flip
+  const float sv = odd ? cr : sr, cv = odd ? -sr : cr;
+  const float s = __uint_as_float(__float_as_uint(sv) ^ (__float_as_uint(x) & 0x80000000u) ^ qs);
+  const float c = __uint_as_float(__float_as_uint(cv) ^ qs);
+  const bool fin = __builtin_isfinite(x);
+  *sp = fin ? s : __builtin_nanf("");
+  *cp = fin ? c : __builtin_nanf("");
+}
 // branch-free (sincos(0) = (0, 1) exactly gives mju_axisAngle2Quat's angle == 0 case); an early
-// return here made the result array a dynamically indexed private array (scratch memory)
+// return here made the result array a dynamically indexed private array (scratch memory).  LIB:
+// the library's sincosf; else sincos_f32 (the same values; the single-step kernel, where it removes
+// the VGPR spills and is 0.8 % faster, while the fused kernel measured 0.3 % slower with it:
+// profiles/AB_LOG.md round 6)
+template <bool LIB = true>
 __device__ __forceinline__ void axisangle2quat(float r[4], const float a[3], float ang) {
   float s, c;
-  sincosf(0.5f * ang, &s, &c);
+  if constexpr (LIB) sincosf(0.5f * ang, &s, &c);
+  else sincos_f32(0.5f * ang, &s, &c);
   r[0] = c; r[1] = a[0] * s; r[2] = a[1] * s; r[3] = a[2] * s;
 }
 // spatial inertia (10-vector about the root subtree com) times a motion vector

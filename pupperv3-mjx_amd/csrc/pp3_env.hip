@@ -230,7 +230,7 @@ __device__ __forceinline__ KinConst kin_const(const DevModel& m, int l) {
   return k;
 }
 
-template <int NC>
+template <int NC, bool LIBSC = true>
 __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int l, bool euler, const KinConst& kc) {
   // lane l < 12 owns leg body (level kl = l / 4, leg gl = l % 4): body bl, joint jl, qpos ql
   const int lc = l < 12 ? l : 11, gl = lc & 3, kl = lc >> 2;
@@ -279,7 +279,7 @@ __device__ __forceinline__ void kinematics(Shared<NC>& s, const DevModel& m, int
   float lq[4] = {1, 0, 0, 0};
   {
     float qloc[4];
-    axisangle2quat(qloc, aax, ang);
+    axisangle2quat<LIBSC>(qloc, aax, ang);
     if (l < 12) mulquat(lq, bq, qloc);
     if (euler && l == 15) {
       normalize4(qb);
@@ -1394,7 +1394,7 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // one physics substep (mj_step): forward + Newton + Euler.  `integrate` = false for reset
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
-template <int NC, int NWV = 1>
+template <int NC, int NWV = 1, bool LIBSC = true>
 __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev,
                                        const KinConst& kc PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
@@ -1416,7 +1416,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
     for (int k = 0; k < 3; k++)
       for (int c = 0; c < 4; c++) rm_pf.f[4 * k + c] = v[2 + k][c];
   }
-  kinematics(s, m, l, integrate_prev, kc); SYNC();
+  kinematics<NC, LIBSC>(s, m, l, integrate_prev, kc); SYNC();
   PHASE(0); l = opaque_lane(l);
   { com_pos(s, m, l, h, rc_pf); SYNC(); }
   PHASE(1); l = opaque_lane(l);
@@ -2019,7 +2019,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
 
 // ---- phase 8: Euler (eulerdamp disabled) of the last substep of a step (the earlier ones run
 // fused into the next substep's kinematics) ----
-template <int NC>
+template <int NC, bool LIBSC = true>
 __device__ __forceinline__ void euler_step(Shared<NC>& s, const DevModel& m, int l) {
   const float hstep = m.h;
   float vn = 0;
@@ -2035,7 +2035,7 @@ __device__ __forceinline__ void euler_step(Shared<NC>& s, const DevModel& m, int
     const float n = sqrtf(dot3(w, w));
     if (n < MINVAL) { w[0] = 1; w[1] = 0; w[2] = 0; } else { const float in = 1.0f / n; w[0] *= in; w[1] *= in; w[2] *= in; }
     float qr[4], q[4] = {s.qpos[3], s.qpos[4], s.qpos[5], s.qpos[6]};
-    axisangle2quat(qr, w, hstep * n);
+    axisangle2quat<LIBSC>(qr, w, hstep * n);
     normalize4(q);
     mulquat(q, q, qr);
     for (int k = 0; k < 4; k++) s.qpos[3 + k] = q[k];
@@ -2669,13 +2669,14 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     // uniform loads become s_load and the rest global_load (a generic pointer would turn them into flat loads)
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    const int wgt = substep<NC, NWV>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
+    // (the single-step kernel takes sincos_f32, the fused one the library's sincosf: same values)
+    const int wgt = substep<NC, NWV, FUSED>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
     heavy = wgt >= HEAVY_WEIGHT ? 1 : 0;
   }
   if (n_frames > 0) {  // the last substep's Euler step (the others ran inside the next kinematics)
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
-    euler_step(s, *(const DevModel*)mp, l);
+    euler_step<NC, FUSED>(s, *(const DevModel*)mp, l);
     PHASE(9);
   }
   if (heavy) __builtin_amdgcn_s_setprio(3);  // the epilogue: heavy waves, then the younger slot, ahead
