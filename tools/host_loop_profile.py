@@ -39,28 +39,49 @@ def main():
             st = env.step(st, acts[a0 + i])
             _ = st.obs[0, 0]
 
-    t = time.perf_counter()
-    loop(N, 0)
-    dt_loop = (time.perf_counter() - t) / N
-    # floors: device launches from the C ABI, synchronised per step / back to back
     L = env._L
-    env.flush()
     abuf = _lib.DeviceBuffer(acts[0].nbytes, env.device)
     abuf.upload(acts[0])
-    env._before_launch()
-    for _ in range(5):
-        _lib.check(L.pp3_step(env._h, abuf.ptr, None))
-    env.synchronize()
-    t = time.perf_counter()
-    for _ in range(N):
-        _lib.check(env._raw.pp3_step(env._h, abuf.ptr, None))
-        _lib.check(env._raw.pp3_synchronize(env._h))
-    dt_sync = (time.perf_counter() - t) / N
-    t = time.perf_counter()
-    for _ in range(N):
-        _lib.check(env._raw.pp3_step(env._h, abuf.ptr, None))
-    env.synchronize()
-    dt_b2b = (time.perf_counter() - t) / N
+    D = env.observation_size
+    blk = _lib.PinnedBlock(4 * E * (D + 2))
+    dev = blk.device_ptr()
+    R = _lib.load()
+
+    def c_sync(n):  # the same single-step launch from C-ABI calls, a stream sync after each
+        env.flush()
+        env._before_launch()
+        for _ in range(n):
+            _lib.check(R.pp3_step(env._h, abuf.ptr, None))
+            _lib.check(R.pp3_synchronize(env._h))
+
+    def c_out(n):  # what env.step issues: a one-step pp3_rollout storing obs | reward | done into a
+        env.flush()  # page-locked block through its device mapping, + sync
+        env._before_launch()
+        for _ in range(n):
+            _lib.check(R.pp3_rollout(env._h, abuf.ptr, E * 12, 1, C.c_void_p(dev + 4 * E * D),
+                                     C.c_void_p(dev + 4 * E * (D + 1)), C.c_void_p(dev), None))
+            _lib.check(R.pp3_synchronize(env._h))
+
+    def c_b2b(n):
+        env.flush()
+        env._before_launch()
+        for _ in range(n):
+            _lib.check(R.pp3_step(env._h, abuf.ptr, None))
+        env.synchronize()
+
+    # interleaved windows (the workload drifts as the robots fall), per-step wall clock
+    res = {"host loop (step + obs read)": [], "C-ABI pp3_step + sync": [],
+           "C-ABI 1-step pp3_rollout to page-locked outputs + sync": [], "C-ABI pp3_step back to back": []}
+    n = max(10, N // 4)
+    a0 = 0
+    for rep in range(4):
+        t = time.perf_counter(); loop(n, a0); res["host loop (step + obs read)"].append((time.perf_counter() - t) / n)
+        a0 += n
+        st = env._issue(False)
+        t = time.perf_counter(); c_sync(n); res["C-ABI pp3_step + sync"].append((time.perf_counter() - t) / n)
+        t = time.perf_counter(); c_out(n); res["C-ABI 1-step pp3_rollout to page-locked outputs + sync"].append((time.perf_counter() - t) / n)
+        t = time.perf_counter(); c_b2b(n); res["C-ABI pp3_step back to back"].append((time.perf_counter() - t) / n)
+        st = env._issue(False)
     # the host loop under cProfile
     pr = cProfile.Profile()
     pr.enable()
@@ -68,9 +89,8 @@ def main():
     pr.disable()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
-    print(f"host loop (step + obs read): {dt_loop * 1e6:.1f} us/step = {E / dt_loop / 1e6:.2f} M env-steps/s")
-    print(f"C-ABI pp3_step + sync:       {dt_sync * 1e6:.1f} us/step = {E / dt_sync / 1e6:.2f} M")
-    print(f"C-ABI pp3_step back to back: {dt_b2b * 1e6:.1f} us/step = {E / dt_b2b / 1e6:.2f} M")
+    for k, v in res.items():
+        print(f"{k:58s} " + " ".join(f"{x * 1e6:6.1f}" for x in v) + f"  us/step (windows of {n} steps, interleaved)")
     print(s.getvalue())
     env.close()
 
