@@ -23,10 +23,11 @@ from pupperv3_mjx.environment import PupperV3Env, make_keys  # noqa: E402
 
 E = 4096
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+PIPE = (sys.argv[2] != "0") if len(sys.argv) > 2 else True  # the constructor default: the pipeline record on
 
 
 def main():
-    env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=True)
+    env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=PIPE)
     acts = np.random.RandomState(3).uniform(-1, 1, size=(N + 10, E, 12)).astype(np.float32)
     st = env.reset(make_keys(0, E))
     for i in range(10):
