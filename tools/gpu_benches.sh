@@ -18,3 +18,4 @@ run c4_gather --envs 8192 --random-commands --gather --no-cpu-baseline
 run policy_drv --policy 256,128,128 --steps 20 --warmup 5 --no-cpu-baseline
 run policy8192 --policy 256,128,128 --envs 8192 --no-cpu-baseline
 run policy8192_drv --policy 256,128,128 --envs 8192 --steps 20 --warmup 5 --no-cpu-baseline
+run c4_unroll_gather --envs 8192 --random-commands --gather --gather-mode unroll --no-cpu-baseline
