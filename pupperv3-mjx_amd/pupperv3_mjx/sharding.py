@@ -12,7 +12,8 @@ Gathered layout (``pp3_gather``): rank r's ``nmax`` rows of width D + 2 at row r
 the rank's env count zero; ``pack_rows`` is its numpy statement, ``unpack_gathered`` drops the
 padding and returns the global [G, D] / [G] / [G] batch in env-id order.  For a K-step unroll
 (``Comm.gather_rollout`` -> ``pp3_gather_rollout``: one collective per unroll, the trajectory of one
-fused ``pp3_rollout``) rank r's block is [K][nmax][D + 2] at r * K * nmax rows (``pack_traj_rows``).
+fused ``pp3_rollout``) rank r's block is [K][nmax][D + 2] at r * K * nmax rows (``pack_traj_rows``;
+``unpack_gathered_rollout`` returns the global [K, G, D] / [K, G] / [K, G] trajectory).
 """
 from __future__ import annotations
 
@@ -77,6 +78,17 @@ def unpack_gathered(full, global_envs: int, world: int):
     out = np.concatenate(rows, 0)
     D = out.shape[1] - 2
     return out[:, :D], out[:, D], out[:, D + 1]
+
+
+def unpack_gathered_rollout(full, global_envs: int, world: int, nsteps: int):
+    """pp3_gather_rollout's [world][K][nmax][D + 2] rows -> (obs [K, G, D], reward [K, G], done [K, G])
+    in global env order."""
+    nmax = max_shard(global_envs, world)
+    full = np.asarray(full).reshape(world, nsteps, nmax, -1)
+    rows = [full[r, :, :shard_bounds(global_envs, world, r)[1]] for r in range(world)]
+    out = np.concatenate(rows, 1)
+    D = out.shape[2] - 2
+    return out[:, :, :D], out[:, :, D], out[:, :, D + 1]
 
 
 # ------------------------------------------------------------------------------ rendezvous

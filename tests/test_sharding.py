@@ -64,6 +64,14 @@ def _worker(rank, world, port, path, ret):
             o, r, d = sharding.unpack_gathered(full.numpy(), G_ENVS, world)
             if rank == 0:
                 ret["gathered"] = ret["gathered"] + [(o, r, d)]
+        # the hand-over once per unroll (pp3_gather_rollout's layout): the K-step trajectory packed
+        # as [K][nmax][D + 2] and ONE all-gather
+        traj = sharding.pack_traj_rows(*(np.stack([p[i] for p in per_step]) for i in range(3)), nmax)
+        local = torch.from_numpy(traj.reshape(STEPS * nmax, -1))
+        full = torch.empty((world * STEPS * nmax, local.shape[1]), dtype=torch.float32)
+        dist.all_gather_into_tensor(full, local)
+        if rank == 0:
+            ret["traj"] = sharding.unpack_gathered_rollout(full.numpy(), G_ENVS, world, STEPS)
     finally:
         dist.destroy_process_group()
 
@@ -92,6 +100,7 @@ def test_two_rank_gloo_gather_matches_single_process(tmp_path):
         ret = mgr.dict()
         mp.spawn(_worker, args=(2, _free_port(), path, ret), nprocs=2, join=True)
         gathered = list(ret["gathered"])
+        traj = ret["traj"]
     model, cfg, _ = common.env_model_and_config(path)
     acts = np.random.RandomState(5).uniform(-1, 1, size=(STEPS, G_ENVS, 12))
     ref = _rollout(model, cfg, make_keys(0, G_ENVS), acts)
@@ -100,6 +109,11 @@ def test_two_rank_gloo_gather_matches_single_process(tmp_path):
         np.testing.assert_array_equal(go, ro.astype(np.float32))
         np.testing.assert_array_equal(gr, rr.astype(np.float32))
         np.testing.assert_array_equal(gd, rd.astype(np.float32))
+    to, tr, td = traj
+    for t, (ro, rr, rd) in enumerate(ref):
+        np.testing.assert_array_equal(to[t], ro.astype(np.float32))
+        np.testing.assert_array_equal(tr[t], rr.astype(np.float32))
+        np.testing.assert_array_equal(td[t], rd.astype(np.float32))
 
 
 def _rdzv_worker(rank, world, d, ret):
@@ -134,6 +148,24 @@ def test_pack_unpack_ragged():
                            for s, n in (sharding.shard_bounds(G, world, r) for r in range(world))])
     assert full.shape == (world * nmax, D + 2)
     o, r, d = sharding.unpack_gathered(full, G, world)
+    np.testing.assert_array_equal(o, obs)
+    np.testing.assert_array_equal(r, rew)
+    np.testing.assert_array_equal(d, done)
+
+
+def test_pack_unpack_rollout_ragged():
+    """pack_traj_rows per rank, concatenated in rank order (pp3_gather_rollout's [world][K][nmax][D + 2]),
+    then unpack_gathered_rollout: the global K-step trajectory back in env order."""
+    rs = np.random.RandomState(1)
+    G, world, K, D = 11, 4, 5, 72
+    obs = rs.normal(size=(K, G, D)).astype(np.float32)
+    rew = rs.uniform(size=(K, G)).astype(np.float32)
+    done = (rs.uniform(size=(K, G)) < 0.3).astype(np.float32)
+    nmax = sharding.max_shard(G, world)
+    full = np.concatenate([sharding.pack_traj_rows(obs[:, s:s + n], rew[:, s:s + n], done[:, s:s + n], nmax)
+                           for s, n in (sharding.shard_bounds(G, world, r) for r in range(world))])
+    assert full.shape == (world * K, nmax, D + 2)
+    o, r, d = sharding.unpack_gathered_rollout(full, G, world, K)
     np.testing.assert_array_equal(o, obs)
     np.testing.assert_array_equal(r, rew)
     np.testing.assert_array_equal(d, done)
