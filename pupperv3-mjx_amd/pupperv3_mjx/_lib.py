@@ -199,6 +199,8 @@ class PinnedBlock:
         check(load().pp3_host_malloc(max(self.nbytes, 4), C.byref(self.ptr)))
         self.__array_interface__ = {"shape": (self.nbytes // 4,), "typestr": "<f4", "version": 3,
                                     "data": (self.ptr.value, False)}
+        # (a lease's arrays are read-only from the start: no per-view flag update)
+        self._ro_interface = dict(self.__array_interface__, data=(self.ptr.value, True))
         self._dev = None
 
     def device_ptr(self) -> int:
@@ -211,12 +213,11 @@ class PinnedBlock:
 
     @staticmethod
     def take(nbytes: int, pool: list) -> "_BlockRef":
-        """A block from `pool` (a BlockPool of free blocks) or a new one; it returns there when released."""
-        import weakref
+        """A block from `pool` (a BlockPool of free blocks) or a new one, leased: it returns there when
+        the lease and every array made from it have died.  The lease's arrays are read-only (the
+        blocks hold launch outputs the host only reads)."""
         b = pool.pop() if pool else PinnedBlock(nbytes)
-        holder = _BlockRef(b)
-        weakref.finalize(holder, _release, pool, b)
-        return holder
+        return _BlockRef(b, pool)
 
     def free(self) -> None:
         if self.ptr:
@@ -232,12 +233,22 @@ class PinnedBlock:
 
 class _BlockRef:
     """One lease of a PinnedBlock: numpy arrays made from it reference this object, whose death
-    returns the block to its pool."""
+    returns the block to its pool (__del__: reference counting releases it the moment the last
+    array dies, without a weakref.finalize registration per lease)."""
 
-    def __init__(self, block: PinnedBlock):
+    def __init__(self, block: PinnedBlock, pool: list):
         self.block = block
         self.ptr = block.ptr
-        self.__array_interface__ = block.__array_interface__
+        self._pool = pool
+        self.__array_interface__ = block._ro_interface
+
+    def __del__(self):
+        pool, self._pool = self._pool, None
+        if pool is not None:
+            try:
+                _release(pool, self.block)
+            except Exception:  # (interpreter shutdown)
+                pass
 
     def device_ptr(self) -> int:
         return self.block.device_ptr()

@@ -244,11 +244,11 @@ class DeviceState(State):
         """True when every array step() would upload is the very object this state was issued with."""
         if self.__dict__.get("_ready") is not None:  # outputs not yet viewed: nothing can have been assigned
             return True
-        if any(self.__dict__.get(k) is not o for k, o in zip(("obs", "reward", "done"), self._out)):
+        d, o = self.__dict__, self._out
+        if d.get("obs") is not o[0] or d.get("reward") is not o[1] or d.get("done") is not o[2]:
             return False
         if not self.materialized:
             return True
-        d = self.__dict__
         return _same(_identity(d["pipeline_state"], d["info"], d["obs"]), self._ids)
 
 
@@ -885,8 +885,8 @@ class PupperV3Env:
         """(obs, reward, done) read-only views of a filled _traj_block."""
         n, D = self.num_envs, self.observation_size
         flat = np.asarray(lease)
-        return (_ro(flat[:K * n * D].reshape(K, n, D)), _ro(flat[K * n * D:K * n * (D + 1)].reshape(K, n)),
-                _ro(flat[K * n * (D + 1):].reshape(K, n)))
+        return (flat[:K * n * D].reshape(K, n, D), flat[K * n * D:K * n * (D + 1)].reshape(K, n),
+                flat[K * n * (D + 1):].reshape(K, n))  # (read-only: a lease's arrays are)
 
     def _rollout_buffers(self, K: int, outputs: bool) -> list:
         """Device buffers of rollout(): actions for K steps, and with `outputs` the reward, done and
@@ -930,12 +930,12 @@ class PupperV3Env:
         """(obs, reward, done): read-only views of a filled page-locked output block; they keep it
         leased until the last of them dies."""
         n, D = self.num_envs, self.observation_size
-        flat = np.asarray(lease)
-        obs = _ro(flat[:n * D].reshape(n, D))
-        rew = _ro(flat[n * D:n * (D + 1)])
-        done = _ro(flat[n * (D + 1):])
+        flat = np.asarray(lease)  # (read-only, and so every view of it)
+        obs = flat[:n * D].reshape(n, D)
+        rew = flat[n * D:n * (D + 1)]
+        done = flat[n * (D + 1):]
         if single:
-            obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
+            obs, rew, done = obs[0], rew[0], done[0]
         return obs, rew, done
 
     def _issue(self, single: bool, lease=None, slot=None) -> DeviceState:
@@ -1102,12 +1102,12 @@ class _StepBatch:
     def views(self, j: int, single: bool):
         """(obs, reward, done) read-only views of step j's rows; they keep the block leased."""
         n, D, B = self.n_envs, self.D, self.cap
-        flat = np.asarray(self.lease)
-        obs = _ro(flat[j * n * D:(j + 1) * n * D].reshape(n, D))
-        rew = _ro(flat[B * n * D + j * n:B * n * D + (j + 1) * n])
-        done = _ro(flat[B * n * (D + 1) + j * n:B * n * (D + 1) + (j + 1) * n])
+        flat = np.asarray(self.lease)  # (read-only, and so every view of it)
+        obs = flat[j * n * D:(j + 1) * n * D].reshape(n, D)
+        rew = flat[B * n * D + j * n:B * n * D + (j + 1) * n]
+        done = flat[B * n * (D + 1) + j * n:B * n * (D + 1) + (j + 1) * n]
         if single:
-            obs, rew, done = _ro(obs[0]), _ro(rew[0]), _ro(done[0])
+            obs, rew, done = obs[0], rew[0], done[0]
         return obs, rew, done
 
 
@@ -1144,13 +1144,17 @@ class _ActSlot:
         ev = C.c_void_p()
         _lib.check(self._L.pp3_event_create(env._h, C.byref(ev)))
         self.ev = ev
+        self.pending = False  # recorded and not yet seen complete
 
     def record(self) -> None:
         _lib.check(self._L.pp3_event_record(self._h, self.ev))
+        self.pending = True
 
     def wait(self) -> None:
-        if self.ev:
+        """Until the recorded launch has completed (no library call when a wait already saw it)."""
+        if self.pending and self.ev:
             _lib.check(self._L.pp3_event_synchronize(self.ev))
+            self.pending = False
 
     def close(self) -> None:
         if self.ev:
