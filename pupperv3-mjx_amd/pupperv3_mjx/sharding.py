@@ -1,7 +1,7 @@
 """Env sharding across GPUs (one process per GPU) and the learner-batch collective.
 
 SURVEY.md 8(e): envs are independent, so a global batch of G envs is cut into contiguous
-per-rank shards with no collective inside the step.  Env i of the global batch gets the same
+per-rank shards (at wave pairs: ``shard_bounds``) with no collective inside the step.  Env i of the global batch gets the same
 PRNG key (``jax.random.split(PRNGKey(seed), G)[i]``) whatever the world size, so a sharded run
 reproduces the single-GPU run env-for-env.  The only collective is the optional per-step
 hand-over of ``obs | reward | done`` to the learner: ``Comm.gather`` -> ``pp3_gather`` (RCCL over
@@ -28,11 +28,23 @@ from . import rng
 
 
 def shard_bounds(global_envs: int, world: int, rank: int) -> Tuple[int, int]:
-    """(first env id, env count) of `rank`'s contiguous shard; the remainder goes to low ranks."""
+    """(first env id, env count) of `rank`'s contiguous shard, cut at wave pairs: envs 2p and 2p + 1
+    share one wave of the step kernel, and a wave with a leg-leg contact in either env takes one
+    Newton factorisation for both, so an env's rounding can depend on its partner.
+    Every shard therefore starts at an even env id: each env keeps the partner it has in the
+    single-GPU batch and a sharded run reproduces that run bit for bit
+    (tests/test_gpu_shard_equivalence.py).  Pairs are dealt with the remainder to the low ranks (rank
+    0's shard is the largest); an odd batch's last pair is its lone last env.  With fewer pairs than
+    ranks the cut falls back to single envs."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad rank {rank} for world {world}")
     if global_envs < world:
         raise ValueError(f"{global_envs} envs cannot be sharded over {world} ranks")
+    pairs = (global_envs + 1) // 2
+    if pairs >= world:
+        base, rem = divmod(pairs, world)
+        start = 2 * (rank * base + min(rank, rem))
+        return start, min(2 * (base + (1 if rank < rem else 0)), global_envs - start)
     base, rem = divmod(global_envs, world)
     count = base + (1 if rank < rem else 0)
     start = rank * base + min(rank, rem)

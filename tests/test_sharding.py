@@ -88,6 +88,21 @@ def test_shard_bounds_cover_exactly_once():
         sharding.shard_bounds(1, 2, 0)
 
 
+def test_shards_start_at_wave_pairs():
+    """Every shard starts at an even env id (the step kernel's wave pairs stay whole), rank 0's is
+    the largest, and an even per-rank count E shards E * world envs as E each (the bench)."""
+    for g in (3, 7, 11, 4097, 8192, 8193):
+        for w in (1, 2, 3, 5, 8):
+            if (g + 1) // 2 < w:
+                continue
+            spans = [sharding.shard_bounds(g, w, r) for r in range(w)]
+            assert all(s % 2 == 0 for s, _ in spans), (g, w, spans)
+            assert max(c for _, c in spans) == spans[0][1] == sharding.max_shard(g, w)
+    for w in (1, 2, 3, 8):
+        assert [sharding.shard_bounds(4096 * w, w, r)[1] for r in range(w)] == [4096] * w
+    assert [sharding.shard_bounds(8192, 3, r) for r in range(3)] == [(0, 2732), (2732, 2730), (5462, 2730)]
+
+
 def test_shard_keys_are_global_key_rows():
     full = make_keys(3, 10)
     rows = np.concatenate([sharding.shard_keys(3, 10, 4, r) for r in range(4)])
