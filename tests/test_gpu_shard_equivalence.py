@@ -48,3 +48,4 @@ def test_shards_reproduce_the_full_batch(require_gpu, world):
         axis = 1 if name.startswith("trajectory") else 0
         joined = np.concatenate([p[k] for p in parts], axis=axis)
         np.testing.assert_array_equal(joined.view(np.uint32), full[k].view(np.uint32), err_msg=name)
+
