@@ -574,7 +574,10 @@ def main():
         env.set_terrain(terrain)
     if args.auto_reset > 0:
         _lib.check(L.pp3_set_auto_reset(env._h, args.auto_reset))
-    keys = sharding.shard_keys(args.seed, E * world, world, rank)  # global env ids, contiguous shards
+    # global env ids: rank r steps envs [r E, (r + 1) E) of the job's E * world (weak scaling: E per
+    # rank, whatever E's parity; sharding.shard_bounds cuts the same ranges when E is even)
+    from pupperv3_mjx import rng as _rng
+    keys = np.ascontiguousarray(_rng.split(_rng.PRNGKey(args.seed), E * world)[rank * E:(rank + 1) * E])
     st = env.reset(keys)
     rec = st._record.copy()
     if not args.random_commands:
