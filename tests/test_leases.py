@@ -65,3 +65,31 @@ def test_retired_pool_frees_a_block_released_later():
     del arr
     gc.collect()
     assert blk.freed and len(pool) == 0
+
+
+def test_action_slot_waits_once_per_record():
+    """An action staging slot synchronizes its completion event once per record: a wait that
+    already saw the launch complete is not repeated (the host loop's ring reuse)."""
+    from pupperv3_mjx.environment import _ActSlot
+    calls = []
+
+    class FakeLib:
+        def pp3_event_record(self, h, ev):
+            calls.append("record")
+            return 0
+
+        def pp3_event_synchronize(self, ev):
+            calls.append("sync")
+            return 0
+
+    slot = object.__new__(_ActSlot)
+    slot._L, slot._h, slot.ev, slot.pending = FakeLib(), None, C.c_void_p(1), False
+    slot.wait()
+    assert calls == []  # never recorded: nothing to wait for
+    slot.record()
+    slot.wait()
+    slot.wait()
+    assert calls == ["record", "sync"]
+    slot.record()
+    slot.wait()
+    assert calls == ["record", "sync", "record", "sync"]
