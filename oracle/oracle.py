@@ -25,7 +25,8 @@ def build() -> None:
 def lib(precision: str = "f64") -> C.CDLL:
     name = {"f64": "liboracle64.so", "f32": "liboracle32.so"}[precision]
     if name not in _LIBS:
-        path = os.path.join(_HERE, name)
+        # PP3_ORACLE_DIR: a sanitizer build of the same sources (tools/oracle_sanitize.sh)
+        path = os.path.join(os.environ.get("PP3_ORACLE_DIR") or _HERE, name)
         if not os.path.exists(path):
             build()
         L = C.CDLL(path)
