@@ -227,7 +227,7 @@ def test_results_independent_of_batch_layout(box_path):
     and dones whether the envs run in one handle or split over two handles (the sharded
     multi-GPU layout; shards start at even env ids, so wave partners are unchanged).  An odd
     split changes wave partners; then an env whose partner has a leg-leg contact takes the dense
-    factorisation with it and may differ at the rounding level."""
+    factorisation with it and may differ at the rounding level ("Wave partners")."""
     n, split = 64, 32
     kw = common.fixture_kwargs(box_path, terminal_body_z=0.0, kick_probability=0.5)
     full = PupperV3Env(**kw, num_envs=n)
