@@ -365,6 +365,47 @@ def test_step_batches_match_synchronous_steps(require_gpu, keep, wrapped):
         environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = saved
 
 
+def test_step_batches_capped_by_block_bytes(require_gpu):
+    """STEP_BLOCK_MAX_BYTES bounds a queued batch's page-locked output block ([B][N][36H + 2]
+    floats): with room for three rows, 8 queued steps run as batches of 3, 3 and 2 steps, still bit
+    for bit the synchronous loop (advisor r05: long observation histories at 4096 envs)."""
+    from pupperv3_mjx import environment
+    saved = (environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH,
+             environment.STEP_BLOCK_MAX_BYTES)
+    acts = np.random.RandomState(16).uniform(-1, 1, size=(8, N, 12)).astype(np.float32)
+    try:
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH = False, False
+        e = _env()
+        st = e.reset(make_keys(17, N))
+        ref = []
+        for t in range(8):
+            st = e.step(st, acts[t])
+            ref.append((np.array(st.obs), np.array(st.reward), np.array(st.done), np.array(st._record)))
+        e.close()
+        environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH = True, True, 16
+        e = _env()
+        environment.STEP_BLOCK_MAX_BYTES = 3 * 4 * N * (e.observation_size + 2) + 1
+        st = e.reset(make_keys(17, N))
+        batches = []
+        for t in range(8):
+            st = e.step(st, acts[t])
+            if not batches or batches[-1] is not e._qb:
+                batches.append(e._qb)
+        np.testing.assert_array_equal(st._record, ref[-1][3])
+        assert [b.cap for b in batches] == [3, 3, 3] and [b.n for b in batches] == [3, 3, 2]
+        t = -1
+        for b in batches:
+            t += b.n
+            go, gr, gd = b.views(b.n - 1, False)
+            np.testing.assert_array_equal(go, ref[t][0])
+            np.testing.assert_array_equal(gr, ref[t][1])
+            np.testing.assert_array_equal(gd, ref[t][2])
+        e.close()
+    finally:
+        (environment.ASYNC_STEP, environment.DEFER_LAUNCH, environment.STEP_BATCH,
+         environment.STEP_BLOCK_MAX_BYTES) = saved
+
+
 def test_dropped_states_get_no_host_rows(require_gpu):
     """LIVE_OUTPUTS_ONLY: a queue of steps whose states the caller dropped is issued as one launch
     without trajectory outputs plus a one-step launch that stores the last state's obs / reward /
