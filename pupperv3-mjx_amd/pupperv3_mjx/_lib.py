@@ -180,7 +180,7 @@ class BlockPool(list):
 
 
 def _release(pool, block) -> None:
-    """weakref finalizer of a lease: the block goes back to its pool (or is freed there)."""
+    """A released lease (_BlockRef.__del__): the block goes back to its pool (or is freed there)."""
     if isinstance(pool, BlockPool):
         pool.release(block)
     else:
