@@ -776,14 +776,15 @@ class PupperV3Env:
         try:
             for e in ends:
                 self._before_launch()
+                # (device addresses as plain ints: the c_void_p argtypes convert them)
                 if LIVE_OUTPUTS_ONLY and e > start:  # steps start .. e-1: dropped states, no host rows
-                    _lib.check(self._raw.pp3_rollout(self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU),
+                    _lib.check(self._raw.pp3_rollout(self._h, act_dev + 4 * start * n * _abi.NU,
                                                      n * _abi.NU, e - start, None, None, None, None))
                     start = e
                 _lib.check(self._raw.pp3_rollout(
-                    self._h, C.c_void_p(act_dev + 4 * start * n * _abi.NU), n * _abi.NU, e - start + 1,
-                    C.c_void_p(dev + 4 * (B * n * D + start * n)), C.c_void_p(dev + 4 * (B * n * (D + 1) + start * n)),
-                    C.c_void_p(dev + 4 * start * n * D), None))
+                    self._h, act_dev + 4 * start * n * _abi.NU, n * _abi.NU, e - start + 1,
+                    dev + 4 * (B * n * D + start * n), dev + 4 * (B * n * (D + 1) + start * n),
+                    dev + 4 * start * n * D, None))
                 for j in range(start if not LIVE_OUTPUTS_ONLY else e, e + 1):
                     qb.stored[j] = True
                 self._gen = qb.gen0 + e + 1
@@ -1088,7 +1089,7 @@ class _StepBatch:
     def __init__(self, env: "PupperV3Env", slot, lease, cap: int):
         n = env.num_envs
         self.slot, self.lease, self.cap = slot, lease, cap
-        self.act = slot.arr[:cap * n * _abi.NU].reshape(cap, n, _abi.NU)
+        self.act = slot.act_rows(cap, n)
         self.n_envs, self.D = n, env.observation_size
         self.gen0 = env._gen
         self.states = []  # weak references to the queued states, in order
@@ -1145,6 +1146,14 @@ class _ActSlot:
         _lib.check(self._L.pp3_event_create(env._h, C.byref(ev)))
         self.ev = ev
         self.pending = False  # recorded and not yet seen complete
+        self._rows = {}
+
+    def act_rows(self, cap: int, n: int) -> np.ndarray:
+        """The block as [cap][n][12] action rows (one view per shape, reused by every batch)."""
+        v = self._rows.get((cap, n))
+        if v is None:
+            v = self._rows[(cap, n)] = self.arr[:cap * n * _abi.NU].reshape(cap, n, _abi.NU)
+        return v
 
     def record(self) -> None:
         _lib.check(self._L.pp3_event_record(self._h, self.ev))
