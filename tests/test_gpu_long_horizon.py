@@ -1,7 +1,8 @@
 """Long horizon at the headline geometry: 4096 envs, random commands, on-device auto-reset
 (episode length 500), U(-1,1) actions, 5000 env steps as fused 100-step rollouts -- ten episodes
-per env slot, with falls, terminations and truncations along the way; flat, and with configs[2]'s
-domain randomisation (the oracle step then runs on each sampled env's own DR row).
+per env slot, with falls, terminations and truncations along the way; flat, with configs[2]'s
+domain randomisation, and with per-env terrain (10 box slots, 5-10 boxes per env; the oracle step
+then runs on each sampled env's own DR row or boxes).
 
 Per rollout, over every env and step of the trajectory: obs / reward / done finite, |obs| within
 the clip, done in {0, 1}, reward in range.  At the end: the state record finite, base quaternions
@@ -24,16 +25,28 @@ pytestmark = pytest.mark.gpu
 N, K, CHUNKS, EPISODE = 4096, 100, 50, 500
 
 
-@pytest.mark.parametrize("dr", [False, True], ids=["flat", "dr"])
-def test_5000_steps_with_auto_reset(require_gpu, dr):
-    e = PupperV3Env(**bench_kwargs(MODEL_XML, True), num_envs=N)
+@pytest.mark.parametrize("variant", ["flat", "dr", "terrain"])
+def test_5000_steps_with_auto_reset(require_gpu, tmp_path, variant):
+    model_path = MODEL_XML
+    if variant == "terrain":  # per-env terrain: 10 box slots, 5-10 boxes of each env's own
+        import xml.etree.ElementTree as ET
+        from pupperv3_mjx import obstacles
+        tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
+        obstacles.add_boxes_to_model(tree, n_boxes=10, x_range=(-5, 5), y_range=(-5, 5), height=0.02, length=6.0)
+        model_path = str(tmp_path / "terrain.xml")
+        tree.write(model_path, encoding="unicode")
+    e = PupperV3Env(**bench_kwargs(model_path, True), num_envs=N)
     try:
-        table = None
-        if dr:  # configs[2]'s domain randomisation, one model row per env
+        table = terrain = None
+        if variant == "dr":  # configs[2]'s domain randomisation, one model row per env
             from pupperv3_mjx import domain_randomization, rng
             sysb, _ = domain_randomization.domain_randomize(e.sys, rng.split(rng.PRNGKey(1000), N))
             e.set_domain_randomization(sysb)
             table = sysb.dr_table().astype(np.float64)
+        if variant == "terrain":
+            from pupperv3_mjx import obstacles
+            terrain = obstacles.sample_terrain(N, 10, (-5, 5), (-5, 5), height=0.02, length=6.0, seed=21, min_boxes=5)
+            e.set_terrain(terrain)
         env = wrappers.wrap(e, episode_length=EPISODE)
         st = env.reset(make_keys(21, N))
         rs = np.random.RandomState(21)
@@ -55,8 +68,8 @@ def test_5000_steps_with_auto_reset(require_gpu, dr):
         assert np.all(ep[:, _abi.EP_STEPS] <= EPISODE)  # every counter restarted within its episode
         # the 5000 steps crossed episode ends: terminations (falls) and truncations (length 500)
         assert dones > N, dones
-        err, _ = one_step_err(e, n_sample=64, seed=7, dr_table=table, auto_reset=True)
-        G.report("long_horizon_5000" + ("_dr" if dr else ""), {"envs": N, "steps": K * CHUNKS, "episode_length": EPISODE, "done_env_steps": dones,
+        err, _ = one_step_err(e, n_sample=64, seed=7, dr_table=table, terrain=terrain, auto_reset=True)
+        G.report("long_horizon_5000_" + variant, {"envs": N, "steps": K * CHUNKS, "episode_length": EPISODE, "done_env_steps": dones,
                                        "one_step_vs_fp64": {k: err[k] for k in ("envs", "constraint_flip_envs",
                                                                                 "auto_reset_envs_excluded",
                                                                                 "qpos_abs_max_unflagged",
