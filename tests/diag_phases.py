@@ -32,10 +32,24 @@ def main():
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     steps = 20
     warm = int(os.environ.get("DIAG_WARMUP", "5"))  # 5: the driver's window (robots landing); 200: steady state
-    env = PupperV3Env(**bench.bench_kwargs(MODEL_XML), num_envs=E, pipeline_output=False)
+    nobst = int(os.environ.get("DIAG_OBST", "0"))  # configs[4]: bench.py --obstacles N (robots started over the boxes)
+    model_path = MODEL_XML
+    if nobst:
+        import tempfile
+        import xml.etree.ElementTree as ET
+        from pupperv3_mjx import obstacles
+        tree = ET.ElementTree(ET.fromstring(open(MODEL_XML).read()))
+        obstacles.add_boxes_to_model(tree, n_boxes=nobst, x_range=(-5, 5), y_range=(-5, 5), height=0.02, length=6.0)
+        model_path = os.path.join(tempfile.mkdtemp(), "obstacles.xml")
+        tree.write(model_path, encoding="unicode")
+    env = PupperV3Env(**bench.bench_kwargs(model_path), num_envs=E, pipeline_output=False)
     st = env.reset(make_keys(0, E))
     rec = st._record.copy()
     rec[:, _abi.S_COMMAND:_abi.S_COMMAND + 3] = [0.5, 0.0, 0.0]  # bench workload (configs[1])
+    if nobst:
+        from pupperv3_mjx import obstacles
+        specs = obstacles.sample_boxes(nobst, (-5, 5), (-5, 5), 0.02, length=6.0)
+        rec[:, _abi.S_QPOS:_abi.S_QPOS + 2] = obstacles.rail_start_xy(specs, E, seed=0)
     env._put(_abi.F_STATE, rec)
     L = env._L
     acts = _lib.DeviceBuffer((steps + warm) * E * 48)
