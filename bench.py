@@ -871,6 +871,8 @@ def main():
         # the library reports which path pp3_rollout_policy took (fused only at cap 8, action_repeat 1,
         # PP3_POLICY_UNFUSED unset and in a product build)
         fused_policy = policy is not None and L.pp3_rollout_policy_fused(env._h) == 1
+        # the step kernels' sphere-box cull (obstacle models): the CULL = true instantiation
+        cull = "true" if hasattr(L, "pp3_narrow_cull") and L.pp3_narrow_cull(env._h) == 1 else "false"
         spl = K if (rollout or fused_policy) else 1  # env steps per launch
         bpe = algorithmic_bytes_per_env_step(env.stride, env._observation_history, args.dr,
                                              trajectory=rollout or policy is not None)
@@ -933,8 +935,9 @@ def main():
             "idle_start": idle_start,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "kernel": ("pp3::env_step_kernel<8, true, 8> (policy MLP fused)" if fused_policy else
-                                    "pp3::env_step_kernel<%d, %s, 1>" % (env.config_struct.ncon_max or 8, "true" if rollout else "false")),
+                         "kernel": ("pp3::env_step_kernel<8, true, 8, %s> (policy MLP fused)" % cull if fused_policy else
+                                    "pp3::env_step_kernel<%d, %s, 1, %s>" % (env.config_struct.ncon_max or 8, "true" if rollout else "false",
+                                                                             cull)),
                          "steps_per_launch": spl, "bytes_per_env_step": bpe,
                          "algorithmic_bytes_per_launch": bpe * E * spl,
                          "launch_ms": round(launch_s * spl * 1e3, 4),

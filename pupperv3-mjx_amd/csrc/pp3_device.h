@@ -210,6 +210,13 @@ struct DevModel {
   // pipeline record only (after everything the step reads)
   LaneTab<(LS_WORDS + 3) / 4> lane_sens;
   float pair_gid[PP3_MAX_PAIR][2];  // MuJoCo geom ids of the pair's two geoms (contact geom fields)
+  // sphere-box cull of the narrow phase (collision): the pairs after the first 32 whose box lies
+  // out of the robot's reach are not evaluated.  Exact: such a pair cannot come within its
+  // margin, so the narrow phase would return no contact for it (the contact set is unchanged)
+  int32_t cull_on;            // 1 <= nbox <= 32, 32 < npair <= 160, every robot geom below body 1
+  float cull_reach;           // >= |sphere centre - body-1 origin| + radius + margin, + 1 cm slack
+  uint32_t pair_box4[32];     // lane l, byte k: box slot of pair 32 (k + 1) + l (0xFF: not sphere-box)
+  TerrainRec box_tab[32];     // static boxes by slot, in the per-env terrain row layout
 };
 
 // ------------------------------- float helpers -------------------------------

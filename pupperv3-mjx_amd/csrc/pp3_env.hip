@@ -637,17 +637,28 @@ __device__ __forceinline__ void store_contact(Shared<NC>& s, const v4f& pc0, int
 // NC pairs penetrate, the NC deepest are kept (same rule as the oracle).  Returns lane c's
 // contact support (pair_sup of contact c; 4 = no contact): the Newton phases read contact
 // supports with v_readlane from this register instead of LDS round trips per contact.
-template <int NC, int NWV = 1>
+// position of the r-th (0-based) set bit of m; r < popc(m)
+__device__ __forceinline__ int nth_bit(uint32_t m, int r) {
+  int pos = 0, c = __popc(m & 0xFFFFu);
+  if (r >= c) { r -= c; m >>= 16; pos += 16; }
+  c = __popc(m & 0xFFu);
+  if (r >= c) { r -= c; m >>= 8; pos += 8; }
+  c = __popc(m & 0xFu);
+  if (r >= c) { r -= c; m >>= 4; pos += 4; }
+  c = __popc(m & 0x3u);
+  if (r >= c) { r -= c; m >>= 2; pos += 2; }
+  return pos + (r >= (int)(m & 1u) ? 1 : 0);
+}
+
+template <int NC, int NWV = 1, bool CULL = false>
 __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h, const PairLoad& pre) {
   int nhit = 0;
   const TerrainRef tr{m.terrain, m.nbox};
-  for (int base = 0; base < m.npair; base += HW) {
-    const int p = base + l;
+  // (cull path) narrow phase of pair p on this lane (p < 0: none), hits compacted in lane order
+  auto run = [&](int p, const PairLoad& pl) {
     float dist = 0, pos[3], nrm[3];
     v4f pc0;
-    // the first 32 pairs' records were fetched at the substep start (they arrive during kinematics)
-    const PairLoad pl = base == 0 ? pre : load_pair(m, p < m.npair ? p : 0);
-    const bool hit = narrow<NC, NWV>(s, tr, pl, dist, pos, nrm, pc0) && (p < m.npair);
+    const bool hit = narrow<NC, NWV>(s, tr, pl, dist, pos, nrm, pc0) && p >= 0;
     const uint32_t mask = hballot(hit, h);
     const int slot = nhit + __popc(mask & ((1u << l) - 1u));
     if (hit) {
@@ -655,6 +666,72 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
       if (slot < NHIT) { s.x.a.hit_dist[slot] = dist; s.x.a.hit_pair[slot] = p; }
     }
     nhit += __popc(mask);
+  };
+  if (!CULL || !m.cull_on) {
+    for (int base = 0; base < m.npair; base += HW) {
+      const int p = base + l;
+      float dist = 0, pos[3], nrm[3];
+      v4f pc0;
+      // the first 32 pairs' records were fetched at the substep start (they arrive during kinematics)
+      const PairLoad pl = base == 0 ? pre : load_pair(m, p < m.npair ? p : 0);
+      const bool hit = narrow<NC, NWV>(s, tr, pl, dist, pos, nrm, pc0) && (p < m.npair);
+      const uint32_t mask = hballot(hit, h);
+      const int slot = nhit + __popc(mask & ((1u << l) - 1u));
+      if (hit) {
+        if (slot < NC) store_contact(s, pc0, slot, p, dist, pos, nrm);
+        if (slot < NHIT) { s.x.a.hit_dist[slot] = dist; s.x.a.hit_pair[slot] = p; }
+      }
+      nhit += __popc(mask);
+    }
+  } else {
+    // boxes (DevModel::cull_on): lane b's box record and this lane's pair-box bytes, loaded ahead
+    // of the first batch; the first 32 pairs run as above
+    const int b = l < tr.nbox ? l : 0;
+    v4f bx[4];
+    if (tr.terrain) {
+      typedef __attribute__((address_space(1))) const v4f GF4;
+      const int env_raw = 2 * NWV * blockIdx.x + (threadIdx.x >> 5);
+      const GF4* t = (const GF4*)(uintptr_t)tr.terrain + ((size_t)env_raw * tr.nbox + b) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; k++) bx[k] = t[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) bx[k] = reinterpret_cast<const v4f*>(&m.box_tab[b])[k];
+    }
+    const uint32_t pbox = m.pair_box4[l];
+    run(l < m.npair ? l : -1, pre);
+    // box b is out of reach when body 1's origin lies farther than the reach outside one of its
+    // slabs (box frame: local = R^T (x - c), as in the narrow phase)
+    const float reach = m.cull_reach;
+    const float d0 = s.xpos[1][0] - bx[0][0], d1 = s.xpos[1][1] - bx[0][1], d2 = s.xpos[1][2] - bx[0][2];
+    const float R[9] = {bx[0][3], bx[1][0], bx[1][1], bx[1][2], bx[1][3], bx[2][0], bx[2][1], bx[2][2], bx[2][3]};
+    bool far = false;
+#pragma unroll
+    for (int k = 0; k < 3; k++) far |= fabsf(R[k] * d0 + R[3 + k] * d1 + R[6 + k] * d2) > bx[3][k] + reach;
+    const uint32_t near = hballot(l < tr.nbox && !far, h);
+    // this half's candidates among pairs 32 .. npair - 1 (every non-box pair, the box pairs of
+    // near boxes), in pair order
+    uint32_t cm[4];
+    int total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int p = 32 * (k + 1) + l;
+      const uint32_t bs = (pbox >> (8 * k)) & 0xFFu;
+      const bool c = p < m.npair && (bs >= 32u || ((near >> (bs & 31u)) & 1u));
+      cm[k] = hballot(c, h);
+      total += __popc(cm[k]);
+    }
+    const int rounds = wmax2(total);
+    for (int base = 0; base < rounds; base += HW) {
+      int p = -1, r = base + l;  // this lane's candidate: the r-th set bit over cm[0..3]
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int c = __popc(cm[k]);
+        if (p < 0 && r < c) p = 32 * (k + 1) + nth_bit(cm[k], r);
+        if (p < 0) r -= c;
+      }
+      run(p, load_pair(m, p >= 0 ? p : 0));
+    }
   }
   if (l == 0) { s.nhit = nhit; s.ncon = nhit < NC ? nhit : NC; }
   const bool ovf = nhit > NC;
@@ -1394,7 +1471,7 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // one physics substep (mj_step): forward + Newton + Euler.  `integrate` = false for reset
 // (mj_forward only).  Must be called by all 64 lanes (both halves).
 // ------------------------------------------------------------------------------------
-template <int NC, int NWV = 1, bool LIBSC = true>
+template <int NC, int NWV = 1, bool LIBSC = true, bool CULL = false>
 __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev,
                                        const KinConst& kc PROF_PARAM) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
@@ -1428,7 +1505,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
   int lsup = 4;  // lane c: support of contact c (4 = none)
-  { lsup = collision<NC, NWV>(s, m, l, h, pair_pf); SYNC(); }
+  { lsup = collision<NC, NWV, CULL>(s, m, l, h, pair_pf); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   // the PairCon of contact c = l / 4 for the first batch of phase 13's edge rows (lane e = 4c + k),
   // loaded here unpinned: it arrives during the limit/actuation and M-entry phases
@@ -2459,7 +2536,9 @@ __device__ __noinline__ void policy_mlp_tile(pp3pol::KNet* net, float* act, int 
 #else
 #define PP3_STEP_WPE 2
 #endif
-template <int NC, bool FUSED, int NWV = 1>
+// CULL: models with obstacle boxes (DevModel::cull_on) launch the instantiation with the
+// sphere-box cull of collision() compiled in; the flat model's code is the same without it
+template <int NC, bool FUSED, int NWV = 1, bool CULL = false>
 __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     typename std::conditional<(NWV > 1), PolicyStepArgs, StepArgs>::type a_arg) {
   static_assert(NWV == 1 || (FUSED && NWV == pp3pol::NWAVE), "the policy rollout is fused, one MLP tile per workgroup");
@@ -2670,7 +2749,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
     // (the single-step kernel takes sincos_f32, the fused one the library's sincosf: same values)
-    const int wgt = substep<NC, NWV, FUSED>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
+    const int wgt = substep<NC, NWV, FUSED, CULL>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
     heavy = wgt >= HEAVY_WEIGHT ? 1 : 0;
   }
   if (n_frames > 0) {  // the last substep's Euler step (the others ran inside the next kinematics)
@@ -2962,6 +3041,7 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
 #endif
 }
 
+
 struct ResetArgs {
   const DevModel* m;
   float* state;
@@ -3129,6 +3209,7 @@ struct pp3_env {
   int action_repeat;  // auto-reset mode: launches per wrapper step (1 otherwise)
   float* terrain;  // TerrainRec rows (pp3_set_terrain), null until first set
   int nbox;        // world box-geom slots in the model
+  int cull;        // DevModel::cull_on: steps launch env_step_kernel<..., CULL = true>
   hipEvent_t ev0, ev1;
 };
 
@@ -3498,6 +3579,47 @@ static int build_devmodel(const pp3_model_t* mm, const pp3_env_config_t* c, DevM
     }
     if (mm->cgeom_margin[g1] != 0 || mm->cgeom_margin[g2] != 0) return set_err(PP3_ERR_MODEL, "nonzero geom margins unsupported");
   }
+  {  // sphere-box cull tables (DevModel::cull_on)
+    d->cull_on = 0;
+    d->cull_reach = 0.0f;
+    memset(d->pair_box4, 0xFF, sizeof(d->pair_box4));
+    memset(d->box_tab, 0, sizeof(d->box_tab));
+    bool ok = d->nbox >= 1 && d->nbox <= 32 && d->npair > 32 && d->npair <= 32 * 5 && mm->body_parentid[1] == 0;
+    const char* off = getenv("PP3_NO_CULL");  // tests only: every pair through the narrow phase
+    if (off && off[0] == '1') ok = false;
+    double reach = 0.0, margin = 0.0;
+    for (int sl = 0; ok && sl < d->nrobot_geom; sl++) {  // chain of link offsets from body 1's origin
+      const int g = d->robot_geom[sl];
+      const double* gp = mm->cgeom_pos[g];
+      double dist = sqrt(gp[0] * gp[0] + gp[1] * gp[1] + gp[2] * gp[2]);
+      int b = mm->cgeom_bodyid[g];
+      for (; b > 1; b = mm->body_parentid[b]) {
+        const double* bp = mm->body_pos[b];
+        dist += sqrt(bp[0] * bp[0] + bp[1] * bp[1] + bp[2] * bp[2]);
+      }
+      if (b != 1) ok = false;
+      reach = fmax(reach, dist + mm->cgeom_size[g][0]);
+    }
+    for (int p = 0; ok && p < d->npair; p++) {
+      const int g1 = mm->pair_g1[p], g2 = mm->pair_g2[p];
+      const bool sb = mm->cgeom_type[g1] == PP3_GEOM_SPHERE && mm->cgeom_type[g2] == PP3_GEOM_BOX && box_slot[g2] >= 0;
+      if (sb) margin = fmax(margin, (double)d->pair_margin[p]);
+      if (p >= 32 && sb) {
+        const int k = p / 32 - 1, ln = p % 32;
+        d->pair_box4[ln] = (d->pair_box4[ln] & ~(0xFFu << (8 * k))) | ((uint32_t)box_slot[g2] << (8 * k));
+      }
+    }
+    for (int g = 0; ok && g < mm->ncgeom; g++) {
+      if (box_slot[g] < 0) continue;
+      TerrainRec& t = d->box_tab[box_slot[g]];
+      for (int k = 0; k < 3; k++) { t.p[k] = d->cg_pos[g][k]; t.half[k] = d->cg_size[g][k]; }
+      for (int k = 0; k < 9; k++) t.R[k] = d->cg_wmat[g][k];
+    }
+    if (ok) {
+      d->cull_reach = (float)(reach + margin + 0.01);
+      d->cull_on = 1;
+    }
+  }
   d->nsite = mm->nsite;
   for (int s = 0; s < mm->nsite; s++) {
     d->site_body[s] = mm->site_bodyid[s];
@@ -3652,6 +3774,7 @@ int pp3_create(const pp3_model_t* model, const pp3_env_config_t* cfg, int32_t nu
   e->stride = hm.stride;
   e->H = hm.H;
   e->nbox = hm.nbox;
+  e->cull = hm.cull_on;
   {
     // contact cap: 8 deepest per env by default, flat or with obstacle boxes (the reference's
     // MJX keeps max_contact_points = 5, test_pupper_model.xml:227-230); 16 on request
@@ -3783,7 +3906,15 @@ static int launch_steps(pp3_env_t* e, const float* actions_dev, int64_t action_s
     a.traj_done = traj_done ? traj_done + (one_launch ? 0 : (size_t)t * e->N) : nullptr;
     a.traj_obs = traj_obs ? traj_obs + (one_launch ? 0 : (size_t)t * on) : nullptr;
     for (a.phase = 0; a.phase < a.repeat; a.phase++) {  // action_repeat: the same action, k launches
-      if (fused) {
+      if (e->cull) {
+        if (fused) {
+          if (e->nc == 8) hipLaunchKernelGGL((env_step_kernel<8, true, 1, true>), grid, block, 0, st, a);
+          else hipLaunchKernelGGL((env_step_kernel<16, true, 1, true>), grid, block, 0, st, a);
+        } else {
+          if (e->nc == 8) hipLaunchKernelGGL((env_step_kernel<8, false, 1, true>), grid, block, 0, st, a);
+          else hipLaunchKernelGGL((env_step_kernel<16, false, 1, true>), grid, block, 0, st, a);
+        }
+      } else if (fused) {
         if (e->nc == 8) hipLaunchKernelGGL((env_step_kernel<8, true>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((env_step_kernel<16, true>), grid, block, 0, st, a);
       } else {
@@ -3824,6 +3955,7 @@ static bool policy_rollout_fused(const pp3_env_t* e) {
 }
 
 int32_t pp3_rollout_policy_fused(const pp3_env_t* e) { return e ? (policy_rollout_fused(e) ? 1 : 0) : -1; }
+int32_t pp3_narrow_cull(const pp3_env_t* e) { return e ? (e->cull ? 1 : 0) : -1; }
 
 int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float* actions_dev, float* reward_dev,
                        float* done_dev, float* obs_dev, void* stream) {
@@ -3868,7 +4000,8 @@ int pp3_rollout_policy(pp3_env_t* e, pp3_policy_t* policy, int32_t nsteps, float
     pa.act = actions_dev;
     pa.net = *pp3_policy_net(policy);
     const dim3 grid((e->N + pp3pol::TILE - 1) / pp3pol::TILE), block(WAVE * pp3pol::NWAVE);
-    hipLaunchKernelGGL((env_step_kernel<8, true, pp3pol::NWAVE>), grid, block, 0, st, pa);
+    if (e->cull) hipLaunchKernelGGL((env_step_kernel<8, true, pp3pol::NWAVE, true>), grid, block, 0, st, pa);
+    else hipLaunchKernelGGL((env_step_kernel<8, true, pp3pol::NWAVE>), grid, block, 0, st, pa);
     HIPCHK(hipGetLastError());
     return PP3_OK;
   }

@@ -71,6 +71,9 @@ def load() -> C.CDLL:
     if hasattr(L, "pp3_rollout_policy_fused"):  # (diagnostic query; absent from pre-round-5 builds used in A/B)
         L.pp3_rollout_policy_fused.argtypes = [vp]
         L.pp3_rollout_policy_fused.restype = i32
+    if hasattr(L, "pp3_narrow_cull"):  # (diagnostic query; absent from pre-round-6 builds used in A/B)
+        L.pp3_narrow_cull.argtypes = [vp]
+        L.pp3_narrow_cull.restype = i32
     L.pp3_set_auto_reset.argtypes = [vp, i32]
     L.pp3_set_action_repeat.argtypes = [vp, i32]
     L.pp3_policy_create.argtypes = [i32, i32, i32, vp, vp, vp, C.POINTER(vp)]
@@ -155,7 +158,7 @@ EXPORTED_SYMBOLS = (
 
 # include/pupper_hip_diag.h: diagnostic entry points (per-phase / per-wave clocks of a -DPP3_PHASE_PROF
 # build; the product library exports them only to return PP3_ERR_ARG)
-DIAG_SYMBOLS = ("pp3_phase_profile", "pp3_wave_profile", "pp3_rollout_policy_fused")
+DIAG_SYMBOLS = ("pp3_phase_profile", "pp3_wave_profile", "pp3_rollout_policy_fused", "pp3_narrow_cull")
 
 
 class BlockPool(list):

@@ -521,6 +521,12 @@ def _compile(root: ET.Element, xml: str) -> CompiledModel:
                 continue
             i1, i2 = (a, b) if ga["type"] <= gb["type"] else (b, a)
             pairs.append((i1, i2))
+    # grouped by geom-type pair (plane-sphere, sphere-sphere, sphere-box), geom order within a
+    # group: the robot's own 32 candidates come first whatever boxes follow, so the kernel's first
+    # (prefetched) 32-pair batch is the same with and without obstacles and the box pairs after it
+    # are culled by box (pp3_env.hip collision()).  The order only decides the contacts' (and their
+    # constraint rows') order -- rounding, and ties of the contact cap; the oracle follows it too.
+    pairs.sort(key=lambda ab: (geoms[cg[ab[0]]]["type"], geoms[cg[ab[1]]]["type"]))
     if len(pairs) > _abi.MAX_PAIR:
         raise ValueError("too many collision pairs")
     m.npair = len(pairs)

@@ -32,6 +32,7 @@ def test_diagnostic_entry_points_live_in_their_own_header():
     buf = (C.c_uint64 * 16)()
     assert L.pp3_phase_profile(buf, 16, 0) != 0  # the product build has no profiler
     assert L.pp3_rollout_policy_fused(None) == -1
+    assert L.pp3_narrow_cull(None) == -1
 
 
 def test_library_loads_and_exports_all_symbols():

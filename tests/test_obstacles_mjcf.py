@@ -47,7 +47,12 @@ def test_model_counts():
 def test_obstacle_model_pairs():
     xml = common.model_with_obstacles_xml(10)
     cm = mjcf.load(xml, is_string=True)
-    assert cm.ngeom == 33 and cm.struct.npair == 32 + 80
+    m = cm.struct
+    assert cm.ngeom == 33 and m.npair == 32 + 80
+    # grouped by geom-type pair: the robot's 32 candidates first (the kernel's prefetched batch),
+    # then the sphere-box pairs that pp3_env.hip's collision() culls box by box
+    types = [(m.cgeom_type[m.pair_g1[p]], m.cgeom_type[m.pair_g2[p]]) for p in range(m.npair)]
+    assert types == [(0, 2)] * 8 + [(2, 2)] * 24 + [(2, 6)] * 80
 
 
 def test_invweight_and_mass_matrix_cross_check():

@@ -17,7 +17,7 @@ NAMES = {0: "kinematics", 1: "com", 2: "limit rows", 3: "M+bias+J", 4: "LDL(M)",
 
 def main(path, nmin):
     s = open(path).read()
-    a = re.search(r"^_ZN3pp315env_step_kernelILi8ELb1E(?:Li1E)?EEv\S*:", s, re.M).start()
+    a = re.search(r"^_ZN3pp315env_step_kernelILi8ELb1E(?:Li1E)?(?:Lb0E)?EEv\S*:", s, re.M).start()
     body = [L.strip() for L in s[a:s.index(".Lfunc_end", a)].split("\n")]
     seg = []
     for L in body:

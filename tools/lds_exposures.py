@@ -13,7 +13,7 @@ NAMES = {0: "kinematics", 1: "com", 2: "limit rows", 3: "M+bias+J", 4: "LDL(M)",
 path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/pp3_prof.s"
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 s = open(path).read()
-a = re.search(r"^_ZN3pp315env_step_kernelILi8ELb1E(?:Li1E)?EEv\S*:", s, re.M).start()
+a = re.search(r"^_ZN3pp315env_step_kernelILi8ELb1E(?:Li1E)?(?:Lb0E)?EEv\S*:", s, re.M).start()
 body = [L.strip() for L in s[a:s.index(".Lfunc_end", a)].split("\n")]
 seg, exp = [], Counter()
 tot = 0

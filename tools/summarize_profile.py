@@ -20,7 +20,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNEL = "env_step_kernel<8, true, 1>"  # (the fused policy rollout is <8, true, 8>)
+KERNEL = "env_step_kernel<8, true, 1, false>"  # (the fused policy rollout is <8, true, 8, false>)
 
 
 def _arg(name, default):
@@ -29,7 +29,7 @@ def _arg(name, default):
 
 def _kernel():
     launch = _arg("--launch", "rollout")
-    return {"step": "env_step_kernel<8, false, 1>", "policy": "env_step_kernel<8, true, 8>"}.get(launch, KERNEL)
+    return {"step": "env_step_kernel<8, false, 1, false>", "policy": "env_step_kernel<8, true, 8, false>"}.get(launch, KERNEL)
 
 
 def _pmc(d):
