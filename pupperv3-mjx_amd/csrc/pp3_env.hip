@@ -40,6 +40,7 @@ constexpr int HMAX = 16;    // observation_history limit
 constexpr int OBS_MOVE = (PP3_OBS_DIM * (HMAX - 1) + HW - 1) / HW;
 constexpr int NROBOT_GEOM = 8;  // collidable spheres on moving bodies (LDS table)
 constexpr int NHIT = 64;        // contact-overflow ranking window (hits kept for ranking)
+constexpr float CULL_SLACK = 0.05f;  // collision's cached near-box mask: re-tested after body 1 moves this far (m)
 constexpr float LS_NOISE = 64.0f;  // line-search convergence floor, in roundoffs of alpha (oracle LS_NOISE)
 
 // Phase-local scratch that never lives across a phase boundary it does not own.
@@ -651,7 +652,8 @@ __device__ __forceinline__ int nth_bit(uint32_t m, int r) {
 }
 
 template <int NC, int NWV = 1, bool CULL = false>
-__device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h, const PairLoad& pre) {
+__device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l, int h, const PairLoad& pre,
+                                         float* ccache = nullptr) {
   int nhit = 0;
   const TerrainRef tr{m.terrain, m.nbox};
   // (cull path) narrow phase of pair p on this lane (p < 0: none), hits compacted in lane order
@@ -684,31 +686,46 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
       nhit += __popc(mask);
     }
   } else {
-    // boxes (DevModel::cull_on): lane b's box record and this lane's pair-box bytes, loaded ahead
-    // of the first batch; the first 32 pairs run as above
-    const int b = l < tr.nbox ? l : 0;
-    v4f bx[4];
-    if (tr.terrain) {
-      typedef __attribute__((address_space(1))) const v4f GF4;
-      const int env_raw = 2 * NWV * blockIdx.x + (threadIdx.x >> 5);
-      const GF4* t = (const GF4*)(uintptr_t)tr.terrain + ((size_t)env_raw * tr.nbox + b) * 4;
-#pragma unroll
-      for (int k = 0; k < 4; k++) bx[k] = t[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; k++) bx[k] = reinterpret_cast<const v4f*>(&m.box_tab[b])[k];
-    }
+    // boxes (DevModel::cull_on).  The near-box mask is cached (ccache: body 1's origin at the
+    // test, then the mask's bits; one per env, in LDS) and re-tested
+    // only when body 1's origin has moved more than CULL_SLACK from where it was tested (the
+    // test widens the reach by the slack), i.e. about once per env step
     const uint32_t pbox = m.pair_box4[l];
-    run(l < m.npair ? l : -1, pre);
-    // box b is out of reach when body 1's origin lies farther than the reach outside one of its
-    // slabs (box frame: local = R^T (x - c), as in the narrow phase)
-    const float reach = m.cull_reach;
-    const float d0 = s.xpos[1][0] - bx[0][0], d1 = s.xpos[1][1] - bx[0][1], d2 = s.xpos[1][2] - bx[0][2];
-    const float R[9] = {bx[0][3], bx[1][0], bx[1][1], bx[1][2], bx[1][3], bx[2][0], bx[2][1], bx[2][2], bx[2][3]};
-    bool far = false;
+    const float b0 = s.xpos[1][0], b1 = s.xpos[1][1], b2 = s.xpos[1][2];
+    {
+      const float c0 = b0 - ccache[0], c1 = b1 - ccache[1], c2 = b2 - ccache[2];
+      const bool stale = !(c0 * c0 + c1 * c1 + c2 * c2 <= CULL_SLACK * CULL_SLACK);
+      if (__ballot(stale)) {  // lane b: box b out of reach when body 1's origin lies farther than
+        // the reach outside one of its slabs (box frame: local = R^T (x - c), as in narrow())
+        const int b = l < tr.nbox ? l : 0;
+        v4f bx[4];
+        if (tr.terrain) {
+          typedef __attribute__((address_space(1))) const v4f GF4;
+          const int env_raw = 2 * NWV * blockIdx.x + (threadIdx.x >> 5);
+          const GF4* t = (const GF4*)(uintptr_t)tr.terrain + ((size_t)env_raw * tr.nbox + b) * 4;
 #pragma unroll
-    for (int k = 0; k < 3; k++) far |= fabsf(R[k] * d0 + R[3 + k] * d1 + R[6 + k] * d2) > bx[3][k] + reach;
-    const uint32_t near = hballot(l < tr.nbox && !far, h);
+          for (int k = 0; k < 4; k++) bx[k] = t[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; k++) bx[k] = reinterpret_cast<const v4f*>(&m.box_tab[b])[k];
+        }
+        const float reach = m.cull_reach + CULL_SLACK;
+        const float d0 = b0 - bx[0][0], d1 = b1 - bx[0][1], d2 = b2 - bx[0][2];
+        const float R[9] = {bx[0][3], bx[1][0], bx[1][1], bx[1][2], bx[1][3], bx[2][0], bx[2][1], bx[2][2], bx[2][3]};
+        bool far = false;
+#pragma unroll
+        for (int k = 0; k < 3; k++) far |= fabsf(R[k] * d0 + R[3 + k] * d1 + R[6 + k] * d2) > bx[3][k] + reach;
+        const uint32_t nm = hballot(l < tr.nbox && !far, h);
+        if (l == 0) {  // (both halves refresh: a fresh test is valid whether or not it was due)
+          ccache[0] = b0;
+          ccache[1] = b1;
+          ccache[2] = b2;
+          ccache[3] = __uint_as_float(nm);
+        }
+        SYNC();
+      }
+    }
+    const uint32_t near = __float_as_uint(ccache[3]);
     // this half's candidates among pairs 32 .. npair - 1 (every non-box pair, the box pairs of
     // near boxes), in pair order
     uint32_t cm[4];
@@ -722,14 +739,24 @@ __device__ __forceinline__ int collision(Shared<NC>& s, const DevModel& m, int l
       total += __popc(cm[k]);
     }
     const int rounds = wmax2(total);
-    for (int base = 0; base < rounds; base += HW) {
-      int p = -1, r = base + l;  // this lane's candidate: the r-th set bit over cm[0..3]
+    // this lane's candidate of round `base`: the (base + l)-th set bit over cm[0..3]
+    auto cand = [&](int base) {
+      int p = -1, r = base + l;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int c = __popc(cm[k]);
         if (p < 0 && r < c) p = 32 * (k + 1) + nth_bit(cm[k], r);
         if (p < 0) r -= c;
       }
+      return p;
+    };
+    // the first round's records issued before the first 32 pairs run (they arrive meanwhile)
+    const int p1 = cand(0);
+    const PairLoad pl1 = load_pair(m, p1 >= 0 ? p1 : 0);
+    run(l < m.npair ? l : -1, pre);
+    if (rounds > 0) run(p1, pl1);
+    for (int base = HW; base < rounds; base += HW) {
+      const int p = cand(base);
       run(p, load_pair(m, p >= 0 ? p : 0));
     }
   }
@@ -1473,7 +1500,7 @@ __device__ __attribute__((noinline)) void dense_search(LdsShared<NC>* sp, int l,
 // ------------------------------------------------------------------------------------
 template <int NC, int NWV = 1, bool LIBSC = true, bool CULL = false>
 __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, int h, bool integrate_prev,
-                                       const KinConst& kc PROF_PARAM) {
+                                       const KinConst& kc PROF_PARAM, float* ccache = nullptr) {
   constexpr int NR = (Shared<NC>::NEFC + HW - 1) / HW;  // constraint rows per lane
   l = opaque_lane(l);
   // the com and M-entry phases' lane records, loaded here without a wait: they arrive while
@@ -1505,7 +1532,7 @@ __device__ __forceinline__ int substep(Shared<NC>& s, const DevModel& m, int l, 
   { crb_times_cdof(s, m, l); rne_chain(s, m, l); SYNC(); }
   PHASE(15); l = opaque_lane(l);
   int lsup = 4;  // lane c: support of contact c (4 = none)
-  { lsup = collision<NC, NWV, CULL>(s, m, l, h, pair_pf); SYNC(); }
+  { lsup = collision<NC, NWV, CULL>(s, m, l, h, pair_pf, ccache); SYNC(); }
   PHASE(16); l = opaque_lane(l);
   // the PairCon of contact c = l / 4 for the first batch of phase 13's edge rows (lane e = 4c + k),
   // loaded here unpinned: it arrives during the limit/actuation and M-entry phases
@@ -2565,6 +2592,13 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
   // the loop and kept live across it (SGPR and VGPR spills).  With FUSED false the loop runs once
   // and the kernel compiles to the single-step code it always was.
   int heavy_prev = 0;  // fused: the load flag carries over into the next step's first substep
+  // obstacle models (CULL): per env, collision's cached near-box mask and body 1's origin when it
+  // was tested (its own array: the env blocks' layout stays the flat model's); invalid at launch start
+  __shared__ float cull_cache[CULL ? 2 * NWV : 1][4];
+  if constexpr (CULL) {
+    const int t = (int)threadIdx.x;
+    if ((t & (HW - 1)) == 0) cull_cache[t >> 5][0] = 1.0e30f;
+  }
   for (int it = 0;;) {
 #ifdef PP3_PHASE_PROF
   if (it == 1) pf->n = 0;  // fused launch: the stamp trace holds the second step (a warm one)
@@ -2749,7 +2783,8 @@ __global__ __launch_bounds__(WAVE * NWV, PP3_STEP_WPE) void env_step_kernel(
     const GModel* mp = (const GModel*)(a.m);
     asm volatile("" : "+s"(mp));
     // (the single-step kernel takes sincos_f32, the fused one the library's sincosf: same values)
-    const int wgt = substep<NC, NWV, FUSED, CULL>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG);
+    const int wgt = substep<NC, NWV, FUSED, CULL>(s, *(const DevModel*)mp, l, h, f > 0, kc PROF_ARG,
+                                                  CULL ? cull_cache[alias ? 0 : 2 * wv + h] : nullptr);
     heavy = wgt >= HEAVY_WEIGHT ? 1 : 0;
   }
   if (n_frames > 0) {  // the last substep's Euler step (the others ran inside the next kinematics)
