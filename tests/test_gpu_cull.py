@@ -83,3 +83,28 @@ def test_cull_env_steps_bit_identical(box_path, monkeypatch, terrain):
     finally:
         a.close()
         b.close()
+
+
+def test_cull_policy_rollout_bit_identical(box_path, monkeypatch):
+    """The fused policy rollout (8-wave workgroups, each wave's envs with their own cached near-box
+    masks) on per-env terrain: the same actions and end state with and without the cull."""
+    from pupperv3_mjx import export
+    from test_gpu_policy import _policy
+    n, K = 40, 10
+    a, b = _pair(monkeypatch, box_path, n)
+    dp = export.DevicePolicy(_policy([72, 256, 128, 128, 24], "elu"))
+    try:
+        keys = make_keys(4, n)
+        sa, sb = a.reset(keys), b.reset(keys)
+        t = common.terrain_under(sa._record[:, _abi.S_QPOS:_abi.S_QPOS + 2].astype(np.float64), 10, seed=5)
+        a.set_terrain(t)
+        b.set_terrain(t)
+        sa, ta = a.rollout_policy(sa, dp, K)
+        sb, tb = b.rollout_policy(sb, dp, K)
+        np.testing.assert_array_equal(ta["action"], tb["action"])
+        np.testing.assert_array_equal(sa._record, sb._record)
+        assert sa.pipeline_state.contact.ncon.sum() > 0
+    finally:
+        dp.close()
+        a.close()
+        b.close()
