@@ -34,7 +34,7 @@ int pp3_wave_profile(uint32_t* host_out, int32_t n);
 int32_t pp3_rollout_policy_fused(const pp3_env_t* e);
 
 /* Whether env `e`'s step kernels cull the narrow phase's sphere-box pairs by box (1: the model has
- * 1..32 obstacle boxes and its pairs after the first 32 are all culled box by box, the launches
+ * 1..32 obstacle boxes and at most 160 candidate pairs -- 16 boxes for the Pupper's 8 spheres --, the launches
  * are env_step_kernel<..., CULL = true>; 0: every pair is evaluated, e.g. a flat model or
  * PP3_NO_CULL=1 at creation), -1 = null handle.  The cull is exact (tests/test_gpu_cull.py). */
 int32_t pp3_narrow_cull(const pp3_env_t* e);
