@@ -108,3 +108,14 @@ def test_cull_policy_rollout_bit_identical(box_path, monkeypatch):
         dp.close()
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("nboxes,want", [(0, 0), (1, 1), (16, 1), (17, 0)])
+def test_cull_applies_up_to_160_pairs(require_gpu, tmp_path, nboxes, want):
+    """The cull needs 1..32 boxes and at most 160 candidate pairs (16 boxes for the 8 spheres);
+    other models evaluate every pair (flat ground: the one 32-pair batch)."""
+    e = PupperV3Env(**common.fixture_kwargs(common.write_model(tmp_path, nboxes)), num_envs=2)
+    try:
+        assert e._L.pp3_narrow_cull(e._h) == want
+    finally:
+        e.close()
